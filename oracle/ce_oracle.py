@@ -1,0 +1,228 @@
+"""CPU oracle for the consensus-entropy selection path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may
+import this module.  It is the checker, never the thing measured or shipped: the
+product (``consensus-entropy_amd/ce_amd``) never imports it.
+
+Two layers:
+
+* ``ref_*`` -- the reference's own expressions, verbatim, on numpy/scipy
+  (``amg_test.py:441-445`` mc, ``:451-452`` hc, ``:473-480`` mix,
+  ``:109-117`` hc table).  Used to generate the golden fixtures
+  (tests/golden/gen_golden.py) and as bench.py's CPU baseline.
+* ``oracle_*`` -- thin ctypes wrappers over ``ce_oracle.c``, the C restatement
+  of those expressions (see its header for the algorithm and citations), with
+  the engine's total order (NaN first, entropy descending, lowest index first).
+  tests/test_oracle.py pins it bit for bit against the golden fixtures.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libce_oracle.so")
+_lib = None
+
+F32, F64, BF16 = 0, 1, 2
+
+
+# ---------------------------------------------------------------------------
+# Reference expressions, verbatim (numpy / scipy), amg_test.py
+# ---------------------------------------------------------------------------
+def ref_mc(pred_prob, q):
+    """amg_test.py:441-445 verbatim.  ``pred_prob`` is the list of M [N,C] member
+    frames/arrays.  Returns (q_ind, ent, consensus_prob)."""
+    from scipy.stats import entropy
+
+    consensus_prob = np.mean(np.array(pred_prob), axis=0)
+    ent = entropy(consensus_prob, axis=1)
+    q_ind = np.argsort(ent)[::-1][:q]
+    return q_ind, ent, consensus_prob
+
+
+def ref_hc(consensus_hc, q):
+    """amg_test.py:451-452 verbatim on an [N_h, C] frequency table."""
+    from scipy.stats import entropy
+
+    ent_hc = entropy(consensus_hc, axis=1)
+    q_ind = np.argsort(ent_hc)[::-1][:q]
+    return q_ind, ent_hc
+
+
+def ref_mix(pred_prob, consensus_hc, q):
+    """amg_test.py:473-480: ROW-stack [mc mean; hc table], entropy, top-q."""
+    from scipy.stats import entropy
+
+    consensus_prob_mc = np.mean(np.array(pred_prob), axis=0)
+    mix_consensus = np.concatenate([consensus_prob_mc, np.asarray(consensus_hc)], axis=0)
+    ent_mix = entropy(mix_consensus, axis=1)
+    q_ind = np.argsort(ent_mix)[::-1][:q]
+    return q_ind, ent_mix
+
+
+def ref_vote_table(votes, C=4):
+    """amg_test.py:109-115 on an int8 vote matrix (-1 = missing): per row,
+    Counter over classes, then ``np.round(v / num_anno, 3)``.  Pure-Python loop
+    (small cases only)."""
+    from collections import Counter
+
+    votes = np.asarray(votes)
+    out = np.empty((votes.shape[0], C), dtype=np.float64)
+    for n in range(votes.shape[0]):
+        row = [int(v) for v in votes[n] if 0 <= v < C]
+        cnt = Counter({c: 0 for c in range(C)})
+        cnt.update(row)
+        num_anno = len(row)
+        for c in range(C):
+            out[n, c] = np.round(cnt[c] / num_anno, 3) if num_anno else np.nan
+    return out
+
+
+def ref_quadrant(arousal, valence):
+    """amg_test.py:69-78 verbatim (returns 'Q1'..'Q4')."""
+    if arousal >= 0 and valence >= 0:
+        quad = "Q1"
+    elif arousal > 0 and valence < 0:
+        quad = "Q2"
+    elif arousal <= 0 and valence <= 0:
+        quad = "Q3"
+    elif arousal < 0 and valence > 0:
+        quad = "Q4"
+    return quad
+
+
+def canonical_order(ent, q):
+    """The engine's total order on a numpy entropy vector: NaN first, then
+    entropy descending, then lowest index.  (numpy's own argsort tie order is
+    unspecified; this is the tightened rule.)"""
+    ent = np.asarray(ent, dtype=np.float64)
+    n = ent.shape[0]
+    isn = np.isnan(ent)
+    key = np.where(isn, 0.0, ent)
+    key = np.where(key == 0.0, 0.0, key)  # -0.0 == +0.0
+    order = np.lexsort((np.arange(n), -key, ~isn))
+    return order[:q]
+
+
+# ---------------------------------------------------------------------------
+# C restatement (ce_oracle.c) via ctypes
+# ---------------------------------------------------------------------------
+def build():
+    """Compile ce_oracle.c (gcc) in place."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, i64, i32, dp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double
+        L.ce_ref_committee_entropy.argtypes = [vp, ctypes.c_int, i64, i32, i32, i64, i64, i64, vp, vp]
+        L.ce_ref_committee_entropy.restype = ctypes.c_int
+        L.ce_ref_table_entropy.argtypes = [vp, i64, i32, i64, vp]
+        L.ce_ref_vote_table.argtypes = [vp, i64, i32, i32, i64, vp, vp]
+        L.ce_ref_va_table.argtypes = [vp, i64, i32, vp, vp]
+        L.ce_ref_topq.argtypes = [vp, i64, i32, i64, vp, vp]
+        L.ce_ref_topq.restype = i64
+        L.ce_ref_topq_merge.argtypes = [vp, vp, i64, i32, vp, vp]
+        L.ce_ref_topq_merge.restype = i64
+        L.ce_ref_quadrant.argtypes = [dp, dp]
+        L.ce_ref_entr.argtypes = [dp]
+        L.ce_ref_entr.restype = dp
+        L.ce_ref_row_sum.argtypes = [vp, i64]
+        L.ce_ref_row_sum.restype = dp
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _dtype_code(a):
+    if a.dtype == np.float32:
+        return F32
+    if a.dtype == np.float64:
+        return F64
+    if a.dtype == np.uint16:  # bf16 bit patterns
+        return BF16
+    raise TypeError(f"unsupported dtype {a.dtype}")
+
+
+def oracle_committee_entropy(P, layout="MNC", want_mean=False):
+    """Entropy per item of a committee tensor ([M,N,C] if layout == 'MNC', else
+    [N,M,C]); bf16 is passed as uint16 bit patterns."""
+    P = np.ascontiguousarray(P)
+    if layout == "MNC":
+        M, N, C = P.shape
+        sN, sM, sC = C, N * C, 1
+    else:
+        N, M, C = P.shape
+        sN, sM, sC = M * C, C, 1
+    ent = np.empty(N, dtype=np.float64)
+    mean = np.empty((N, C), dtype=np.float64) if want_mean else None
+    rc = lib().ce_ref_committee_entropy(_ptr(P), _dtype_code(P), N, M, C, sN, sM, sC,
+                                        _ptr(mean) if want_mean else None, _ptr(ent))
+    assert rc == 0
+    return (ent, mean) if want_mean else ent
+
+
+def oracle_table_entropy(T):
+    T = np.ascontiguousarray(T, dtype=np.float64)
+    N, C = T.shape
+    ent = np.empty(N, dtype=np.float64)
+    lib().ce_ref_table_entropy(_ptr(T), N, C, C, _ptr(ent))
+    return ent
+
+
+def oracle_vote_table(votes, C=4):
+    votes = np.ascontiguousarray(votes, dtype=np.int8)
+    N, A = votes.shape
+    freq = np.empty((N, C), dtype=np.float64)
+    ent = np.empty(N, dtype=np.float64)
+    lib().ce_ref_vote_table(_ptr(votes), N, A, C, A, _ptr(freq), _ptr(ent))
+    return freq, ent
+
+
+def oracle_va_table(va):
+    """va: [N, A, 2] float64 (valence, arousal), NaN = missing."""
+    va = np.ascontiguousarray(va, dtype=np.float64)
+    N, A, _ = va.shape
+    freq = np.empty((N, 4), dtype=np.float64)
+    ent = np.empty(N, dtype=np.float64)
+    lib().ce_ref_va_table(_ptr(va), N, A, _ptr(freq), _ptr(ent))
+    return freq, ent
+
+
+def oracle_topq(ent, q, base=0):
+    ent = np.ascontiguousarray(ent, dtype=np.float64)
+    vals = np.empty(max(q, 1), dtype=np.float64)
+    idx = np.empty(max(q, 1), dtype=np.int64)
+    k = lib().ce_ref_topq(_ptr(ent), ent.shape[0], q, base, _ptr(vals), _ptr(idx))
+    return vals[:k], idx[:k]
+
+
+def oracle_topq_merge(vals, idx, q):
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    ov = np.empty(max(q, 1), dtype=np.float64)
+    oi = np.empty(max(q, 1), dtype=np.int64)
+    k = lib().ce_ref_topq_merge(_ptr(vals), _ptr(idx), vals.shape[0], q, _ptr(ov), _ptr(oi))
+    return ov[:k], oi[:k]
+
+
+def oracle_select_mc(P, q, layout="MNC"):
+    ent = oracle_committee_entropy(P, layout)
+    return oracle_topq(ent, q)
+
+
+def oracle_select_mix(P, hc_table, q, layout="MNC"):
+    ent_mc = oracle_committee_entropy(P, layout)
+    ent_hc = oracle_table_entropy(hc_table)
+    return oracle_topq(np.concatenate([ent_mc, ent_hc]), q)
