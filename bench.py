@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark of the consensus-entropy selection path on MI355X.
+
+Metric (BASELINE.json): pool items scored+ranked/sec (M=16, C=4), whole job.
+Workload: BASELINE.json configs[3] -- a 100M-item pool x 16 members x 4 classes,
+fp32 probabilities in the item-major [N, M, C] layout (25.6 GB), q = 10.  It
+fits one MI355X (288 GB), so N=1 runs the whole pool on one GPU; with N GPUs
+the SAME pool is sharded over the ranks (strong scaling, as the north star's
+"6x at 8 GPUs on the 100M-item pool" asks) and the ranks exchange their local
+top-q with one RCCL all-gather before an identical merge on every rank.
+
+One step = the full selection: fused score + per-block top-q over the resident
+shard (stage 1, the streaming kernel), the merge of the blocks' candidates
+(stage 2), and for N > 1 the all-gather + merge.  Inputs are synthetic
+Dirichlet(1) member rows (1% un-normalised, like sigmoid CNN members), seed
+1987, generated on the device before timing.
+
+Also reported:
+  roofline      stage-1 kernel: algorithmic bytes (N_local x 256 B) / its mean
+                duration from HIP events on the launch stream, vs 8 TB/s;
+                traffic = HBM bytes per launch from the committed rocprofv3 PMC
+                pass (profiles/), or null
+  cpu_baseline  the reference's own expressions (amg_test.py:441-445, numpy +
+                scipy) on a bounded sample, rank 0 at N=1 only
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "consensus-entropy_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "pool items scored+ranked/sec (M=16,C=4) at 1/2/4/8 GPUs; % HBM roofline"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_pool(n, M, C, seed, device, chunk=8_000_000):
+    """Dirichlet(1) rows per (item, member); 1% of member rows scaled by U(0.5, 2)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    P = torch.empty((n, M, C), dtype=torch.float32, device=device)
+    for s in range(0, n, chunk):
+        m = min(n, s + chunk) - s
+        e = -torch.log(torch.rand((m, M, C), device=device, generator=g).clamp_min_(1e-30))
+        e /= e.sum(-1, keepdim=True)
+        scale = torch.where(torch.rand((m, M, 1), device=device, generator=g) < 0.01,
+                            torch.rand((m, M, 1), device=device, generator=g) * 1.5 + 0.5,
+                            torch.ones((), device=device))
+        P[s:s + m] = e * scale
+        del e, scale
+    return P
+
+
+def cpu_baseline(n_items, M, C, q, seed=1987):
+    """amg_test.py:441-445 verbatim (numpy/scipy) on n_items; mixed member
+    dtypes like the reference committee (GNB/SGD f64, XGB/CNN f32)."""
+    import numpy as np
+
+    from oracle.ce_oracle import ref_mc
+
+    rng = np.random.default_rng(seed)
+    members = []
+    for m in range(M):
+        e = -np.log(rng.random((n_items, C)))
+        p = e / e.sum(-1, keepdims=True)
+        members.append(p if m < M // 2 else p.astype(np.float32))
+    ref_mc(members, q)  # warm-up
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        ref_mc(members, q)
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts)
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": n_items / t,
+        "unit": "items/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"reference expressions amg_test.py:441-445 verbatim (np.mean(np.array(pred_prob),0), "
+                   f"scipy.stats.entropy(axis=1), np.argsort()[::-1][:{q}]) on {n_items} items x {M} mixed "
+                   f"f64/f32 members x {C} classes; median of 5 after 1 warm-up = {t:.3f} s; numpy "
+                   f"single-threaded; host: {cpu}, {os.cpu_count()} logical cpus visible"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n-items", type=int, default=100_000_000)
+    ap.add_argument("--members", type=int, default=16)
+    ap.add_argument("--classes", type=int, default=4)
+    ap.add_argument("--q", type=int, default=10)
+    ap.add_argument("--layout", default="NMC", choices=["NMC", "MNC"])
+    ap.add_argument("--cpu-sample", type=int, default=6_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import ce_amd
+    from ce_amd import dist as cdist
+    from ce_amd import ops
+
+    ce_amd.load()
+    N, M, C, q = args.n_items, args.members, args.classes, args.q
+    lo, hi = cdist.shard_range(N, rank, world)
+    n_local = hi - lo
+    t0 = time.time()
+    P = make_pool(n_local, M, C, 1987 + rank, device)
+    if args.layout == "MNC":
+        P = P.permute(1, 0, 2).contiguous()
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] pool shard {n_local} x {M} x {C} fp32 ({P.numel() * 4 / 1e9:.1f} GB) "
+        f"generated in {time.time() - t0:.1f}s")
+    plan = ops.MCPlan(P, q, args.layout, base_idx=lo)
+
+    def step():
+        plan.partial()
+        vals, idx = plan.finish()
+        if world > 1:
+            av, ai = cdist.allgather_topq(vals, idx, q)
+            vals, idx = ops.topq_merge(av, ai, q)
+        return vals, idx
+
+    for _ in range(args.warmup):
+        step()
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        plan.partial()
+        ev[k][1].record(stream)
+        vals, idx = plan.finish()
+        if world > 1:
+            av, ai = cdist.allgather_topq(vals, idx, q)
+            vals, idx = ops.topq_merge(av, ai, q)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    kern_ms = statistics.mean(a.elapsed_time(b) for a, b in ev)
+    picks = idx.cpu().tolist()
+
+    if rank == 0:
+        bytes_per_launch = n_local * M * C * P.element_size()
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(TRAFFIC_FILE) as f:
+                tr = json.load(f)
+            key = f"{args.layout}_{N}_{M}_{C}_q{q}_w{world}"
+            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        line = {
+            "metric": METRIC,
+            "value": N * args.steps / elapsed,
+            "unit": "items/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"configs[3] large-ensemble pool: {N} items x {M} members x {C} classes fp32, "
+                             f"[N,M,C] layout={args.layout}, q={q}, sharded over {world} GPU(s)"),
+                "n_items": N, "members": M, "classes": C, "q": q, "input_dtype": "f32",
+                "layout": args.layout, "items_per_gpu": n_local,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS,
+                "traffic": traffic,
+                "kernel": "k_partial<CommitteeSrc<f32,C=4,vec>> (stage 1)",
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+            },
+            "cpu_baseline": None,
+            "selected": picks,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            del P, plan
+            torch.cuda.empty_cache()
+            line["cpu_baseline"] = cpu_baseline(args.cpu_sample, M, C, q)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

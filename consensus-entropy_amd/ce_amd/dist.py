@@ -1,0 +1,68 @@
+"""Multi-GPU selection: the pool's N axis sharded over ranks (one process per GPU).
+
+Each rank scores its contiguous shard [lo, hi) of the pool with the fused
+kernel (positions reported globally: base_idx = lo), the ranks exchange their
+local top-q with ONE all-gather of q x (f64 entropy, i64 position) = 16q bytes
+per rank (RCCL over xGMI when the backend is "nccl"; latency-bound at q = 10),
+and every rank runs the same deterministic merge.  Exact: the global top-q is a
+subset of the union of the local top-qs, and the merge uses the same total
+order (NaN first, entropy descending, lowest position).
+
+The local-select and merge steps are injectable so the collective logic can be
+exercised on CPU with the gloo backend (tests/test_dist.py); by default they
+are the HIP operators.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+
+def shard_range(n, rank, world):
+    """Contiguous shard of n items for `rank` (sizes differ by at most 1)."""
+    base, rem = divmod(int(n), int(world))
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def pack(vals, idx):
+    """(f64 [q], i64 [q]) -> one i64 [2q] tensor (f64 bits viewed as i64)."""
+    return torch.cat([vals.contiguous().view(torch.int64), idx.contiguous()])
+
+
+def unpack(buf, q, world):
+    b = buf.view(world, 2 * q)
+    return b[:, :q].contiguous().view(torch.float64).reshape(-1), b[:, q:].contiguous().reshape(-1)
+
+
+def allgather_topq(vals, idx, q, group=None):
+    """All-gather every rank's best-first (vals, idx) list: returns the
+    concatenated [world*q] lists, rank-major."""
+    world = dist.get_world_size(group)
+    send = pack(vals, idx)
+    recv = torch.empty(world * send.numel(), dtype=send.dtype, device=send.device)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    return unpack(recv, q, world)
+
+
+def sharded_select_mc(P_local, q, *, global_offset, layout="NMC", group=None, local_select=None, merge=None):
+    """Global top-q over the union of every rank's shard.
+
+    P_local        this rank's committee shard (items [global_offset, +n))
+    local_select   f(P_local, q, base_idx) -> (vals [q], idx [q]); default the
+                   fused HIP kernel ops.select_mc
+    merge          f(vals [world*q], idx [world*q], q) -> (vals, idx);
+                   default ops.topq_merge (HIP)
+    """
+    if local_select is None:
+        def local_select(P, qq, base):
+            return ops.select_mc(P, qq, layout, base_idx=base)
+    if merge is None:
+        merge = ops.topq_merge
+    vals, idx = local_select(P_local, q, int(global_offset))
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return vals, idx
+    all_vals, all_idx = allgather_topq(vals, idx, q, group)
+    return merge(all_vals, all_idx, q)

@@ -1,0 +1,227 @@
+"""Device-tensor operators over the C-ABI (torch is plumbing: memory + streams).
+
+Every op takes torch tensors resident on a HIP device, launches on torch's
+current stream and returns device tensors; nothing is synchronised here.
+There is no CPU path: a CPU tensor is an error.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import CE_BF16, CE_F32, CE_F64, call
+
+_DT = {torch.float32: CE_F32, torch.float64: CE_F64, torch.bfloat16: CE_BF16}
+LAYOUTS = ("MNC", "NMC")
+
+
+def _stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _on_gpu(t, what):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{what} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{what} must live on a HIP device (got {t.device}); there is no CPU path")
+
+
+class _WorkspaceCache:
+    """Per-device scratch reused across calls (grows, never shrinks), so steady
+    state allocates nothing."""
+
+    def __init__(self):
+        self._ws = {}
+
+    def get(self, device, nbytes):
+        key = torch.device(device).index
+        buf = self._ws.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self._ws[key] = buf
+        return buf
+
+
+WORKSPACE = _WorkspaceCache()
+
+
+def committee_view(P, layout="MNC"):
+    """(N, M, C, sN, sM, sC, dtype code) of a committee tensor.  'MNC' is the
+    reference's stack np.array(pred_prob) (amg_test.py:441); 'NMC' is the
+    item-major [N, M, C] tensor.  Any strides are accepted."""
+    _on_gpu(P, "committee")
+    if P.dim() != 3:
+        raise ValueError(f"committee must be 3-D, got shape {tuple(P.shape)}")
+    if P.dtype not in _DT:
+        raise TypeError(f"committee dtype {P.dtype} not in float32/float64/bfloat16")
+    if layout == "MNC":
+        M, N, C = P.shape
+        sM, sN, sC = P.stride()
+    elif layout == "NMC":
+        N, M, C = P.shape
+        sN, sM, sC = P.stride()
+    else:
+        raise ValueError(f"layout must be one of {LAYOUTS}, got {layout!r}")
+    if M < 1 or C < 1:
+        raise ValueError(f"committee needs M >= 1 members and C >= 1 classes, got M={M}, C={C}")
+    return N, M, C, sN, sM, sC, _DT[P.dtype]
+
+
+def committee_entropy(P, layout="MNC", return_mean=False):
+    """amg_test.py:441+443 per item: f64 entropies [N] (and the [N, C] mean)."""
+    N, M, C, sN, sM, sC, dt = committee_view(P, layout)
+    ent = torch.empty(N, dtype=torch.float64, device=P.device)
+    mean = torch.empty((N, C), dtype=torch.float64, device=P.device) if return_mean else None
+    call("ce_committee_entropy", _p(P), dt, N, M, C, sN, sM, sC, _p(mean), _p(ent), _stream(P.device))
+    return (ent, mean) if return_mean else ent
+
+
+def vote_table(votes, C=4):
+    """amg_test.py:109-117 on int8 votes [N, A] (-1 = missing): (freq [N, C], ent [N])."""
+    _on_gpu(votes, "votes")
+    if votes.dtype != torch.int8 or votes.dim() != 2:
+        raise ValueError("votes must be a 2-D int8 tensor")
+    if votes.stride(1) != 1:
+        votes = votes.contiguous()
+    N, A = votes.shape
+    freq = torch.empty((N, C), dtype=torch.float64, device=votes.device)
+    ent = torch.empty(N, dtype=torch.float64, device=votes.device)
+    call("ce_vote_entropy", _p(votes), N, A, C, votes.stride(0), _p(freq), _p(ent), _stream(votes.device))
+    return freq, ent
+
+
+def va_table(va):
+    """amg_test.py:88-117 from raw [N, A, 2] f64 (valence, arousal), NaN = missing."""
+    _on_gpu(va, "va")
+    if va.dtype != torch.float64 or va.dim() != 3 or va.shape[2] != 2:
+        raise ValueError("va must be a [N, A, 2] float64 tensor")
+    va = va.contiguous()
+    N, A, _ = va.shape
+    freq = torch.empty((N, 4), dtype=torch.float64, device=va.device)
+    ent = torch.empty(N, dtype=torch.float64, device=va.device)
+    call("ce_va_entropy", _p(va), N, A, _p(freq), _p(ent), _stream(va.device))
+    return freq, ent
+
+
+def _check_q(q):
+    q = int(q)
+    if q < 1 or q > _lib.CE_MAX_Q:
+        raise ValueError(f"q={q} outside [1, {_lib.CE_MAX_Q}]")
+    return q
+
+
+def _outs(q, device, lead=()):
+    return (torch.empty(lead + (q,), dtype=torch.float64, device=device),
+            torch.empty(lead + (q,), dtype=torch.int64, device=device))
+
+
+def topq(ent, q, base_idx=0):
+    """np.argsort(ent)[::-1][:q] under the total order (NaN first, desc, lowest
+    index).  Returns (vals [q], idx [q]); idx = -1 marks empty slots."""
+    _on_gpu(ent, "ent")
+    q = _check_q(q)
+    ent = ent.contiguous().to(torch.float64)
+    N = ent.numel()
+    lib = _lib.load()
+    ws = WORKSPACE.get(ent.device, lib.ce_topq_workspace_bytes(N, q))
+    vals, idx = _outs(q, ent.device)
+    call("ce_topq", _p(ent), N, q, int(base_idx), _p(ws), ws.numel(), _p(vals), _p(idx), _stream(ent.device))
+    return vals, idx
+
+
+def topq_merge(vals, idx, q):
+    """Merge best-first candidate lists of q slots each (e.g. per-GPU top-q
+    after an all-gather) into the global top-q."""
+    _on_gpu(vals, "vals")
+    q = _check_q(q)
+    vals = vals.contiguous().view(-1)
+    idx = idx.contiguous().view(-1)
+    if vals.numel() != idx.numel() or vals.numel() % q:
+        raise ValueError("vals/idx must hold nlists * q entries")
+    ov, oi = _outs(q, vals.device)
+    call("ce_topq_merge", _p(vals), _p(idx), vals.numel() // q, q, _p(ov), _p(oi), _stream(vals.device))
+    return ov, oi
+
+
+def select_mc(P, q, layout="MNC", base_idx=0):
+    """Fused amg_test.py:441-445: (vals [q], idx [q]) best-first."""
+    N, M, C, sN, sM, sC, dt = committee_view(P, layout)
+    q = _check_q(q)
+    lib = _lib.load()
+    ws = WORKSPACE.get(P.device, lib.ce_select_mc_workspace_bytes(N, q))
+    vals, idx = _outs(q, P.device)
+    call("ce_select_mc", _p(P), dt, N, M, C, sN, sM, sC, q, int(base_idx), _p(ws), ws.numel(), _p(vals),
+         _p(idx), _stream(P.device))
+    return vals, idx
+
+
+class MCPlan:
+    """Pre-bound two-stage mc selection (stage 1 = the streaming kernel, stage 2
+    = the merge), with its own workspace and outputs: what the bench and the
+    multi-GPU driver launch every step."""
+
+    def __init__(self, P, q, layout="NMC", base_idx=0):
+        self.P = P
+        self.N, self.M, self.C, self.sN, self.sM, self.sC, self.dt = committee_view(P, layout)
+        self.q = _check_q(q)
+        self.base_idx = int(base_idx)
+        lib = _lib.load()
+        self.ws_bytes = lib.ce_select_mc_workspace_bytes(self.N, self.q)
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=P.device)
+        self.vals, self.idx = _outs(self.q, P.device)
+
+    def partial(self):
+        call("ce_select_mc_partial", _p(self.P), self.dt, self.N, self.M, self.C, self.sN, self.sM, self.sC, self.q,
+             self.base_idx, _p(self.ws), self.ws_bytes, _stream(self.P.device))
+
+    def finish(self):
+        call("ce_select_finish", self.N, self.q, _p(self.ws), self.ws_bytes, _p(self.vals), _p(self.idx),
+             _stream(self.P.device))
+        return self.vals, self.idx
+
+    def __call__(self):
+        self.partial()
+        return self.finish()
+
+
+def select_mix(P, hc, q, layout="MNC"):
+    """Fused amg_test.py:473-480: top-q over the row stack [mc (N); hc (N_h)]."""
+    N, M, C, sN, sM, sC, dt = committee_view(P, layout)
+    _on_gpu(hc, "hc table")
+    if hc.dim() != 2 or hc.shape[1] != C:
+        raise ValueError(f"hc table must be [N_h, {C}]")
+    hc = hc.to(torch.float64)
+    if hc.stride(1) != 1:
+        hc = hc.contiguous()
+    q = _check_q(q)
+    N_h = hc.shape[0]
+    lib = _lib.load()
+    ws = WORKSPACE.get(P.device, lib.ce_select_mix_workspace_bytes(N, N_h, q))
+    vals, idx = _outs(q, P.device)
+    call("ce_select_mix", _p(P), dt, N, M, C, sN, sM, sC, _p(hc), N_h, hc.stride(0), q, _p(ws), ws.numel(),
+         _p(vals), _p(idx), _stream(P.device))
+    return vals, idx
+
+
+def select_batched(P, offsets, q, layout="MNC"):
+    """U users in one launch; user u owns items offsets[u]:offsets[u+1].
+    Returns (vals [U, q], idx [U, q]) with user-local positions."""
+    N, M, C, sN, sM, sC, dt = committee_view(P, layout)
+    _on_gpu(offsets, "offsets")
+    offsets = offsets.to(torch.int64).contiguous()
+    U = offsets.numel() - 1
+    if U < 1:
+        raise ValueError("offsets must hold U + 1 >= 2 entries")
+    q = _check_q(q)
+    lib = _lib.load()
+    ws = WORKSPACE.get(P.device, lib.ce_select_batched_workspace_bytes(N, U, q))
+    vals, idx = _outs(q, P.device, (U,))
+    call("ce_select_batched", _p(P), dt, N, M, C, sN, sM, sC, _p(offsets), U, q, _p(ws), ws.numel(), _p(vals),
+         _p(idx), _stream(P.device))
+    return vals, idx

@@ -1,0 +1,235 @@
+// ce_device.hpp -- device-side arithmetic of the selection path (gfx950).
+//
+// Every routine here restates one piece of the reference's NumPy/SciPy arithmetic
+// in f64, in the same operation order, so that the GPU path reproduces the
+// reference bit for bit wherever the C library's log and the device log agree
+// (see DESIGN.md "Numerics"):
+//   mean      np.mean(np.array(pred_prob), axis=0)        amg_test.py:441
+//   entropy   scipy.stats.entropy(consensus, axis=1)      amg_test.py:443,451,479
+//   hc freq   np.round(count / n_votes, 3)                amg_test.py:115
+//   quadrant  get_quadrant(arousal, valence)              amg_test.py:69-78
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ce {
+
+enum DType : int { kF32 = 0, kF64 = 1, kBF16 = 2 };
+
+// ---------------------------------------------------------------------------
+// Total order of the selection, as an unsigned 64-bit key: larger key = better.
+// NaN -> max (ranked first, as argsort()[::-1] puts NaN first); -0.0 -> +0.0;
+// ties on the key are broken by the lower index (the north-star rule).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t order_key(double h) {
+    if (__builtin_isnan(h)) return ~0ull;
+    const uint64_t b = (uint64_t)__double_as_longlong(h + 0.0);  // -0.0 + 0.0 = +0.0
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double key_to_val(uint64_t k) {
+    if (k == ~0ull) return __longlong_as_double(0x7ff8000000000000ll);
+    const uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+__device__ __forceinline__ bool better(uint64_t ka, int64_t ia, uint64_t kb, int64_t ib) {
+    return ka > kb || (ka == kb && ia < ib);
+}
+
+// scipy.special.entr: NaN -> NaN, x > 0 -> -x*log(x), x == 0 -> 0, x < 0 -> -inf.
+// Branch-free form: for x == 0 and x < 0 the product is replaced, so the
+// log of a non-positive argument never reaches the result.
+__device__ __forceinline__ double entr(double x) {
+    double r = -x * log(x);
+    r = (x == 0.0) ? 0.0 : r;
+    r = (x < 0.0) ? -__builtin_inf() : r;
+    return r;  // NaN input: x==0 and x<0 are false, r = -NaN*log(NaN) = NaN
+}
+
+// ---------------------------------------------------------------------------
+// numpy's pairwise summation (loops_utils.h.src) over a compile-time-sized
+// register array, plus the reduction identity: np.sum(row) == 0.0 + pairwise.
+// ---------------------------------------------------------------------------
+template <int OFF, int N, int TOT>
+__device__ __forceinline__ double pairwise(const double (&a)[TOT]) {
+    if constexpr (N < 8) {
+        double r = -0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) r += a[OFF + i];
+        return r;
+    } else if constexpr (N <= 128) {
+        double r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = a[OFF + j];
+        constexpr int NB = N - (N % 8);
+#pragma unroll
+        for (int i = 8; i < NB; i += 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] += a[OFF + i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+        for (int i = NB; i < N; ++i) res += a[OFF + i];
+        return res;
+    } else {
+        constexpr int H = N / 2;
+        constexpr int N2 = H - (H % 8);
+        return pairwise<OFF, N2, TOT>(a) + pairwise<OFF + N2, N - N2, TOT>(a);
+    }
+}
+
+template <int C>
+__device__ __forceinline__ double row_sum(const double (&a)[C]) {
+    return 0.0 + pairwise<0, C, C>(a);
+}
+
+// scipy.stats.entropy of one row held in registers (mean: consensus row).
+template <int C>
+__device__ __forceinline__ double entropy_row(const double (&mean)[C]) {
+    const double s = row_sum<C>(mean);
+    double e[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) e[c] = entr(1.0 * mean[c] / s);
+    return row_sum<C>(e);
+}
+
+// mean = acc / M as numpy's true_divide; a power-of-two M divides exactly by a
+// multiply with its (exact) reciprocal, which rounds identically.
+__device__ __forceinline__ double div_members(double acc, double dM, double invM, bool pow2) {
+    return pow2 ? acc * invM : acc / dM;
+}
+
+// np.round(count / n, 3) == rint(x * 1000.0) / 1000.0 with x = count / n in f64.
+__device__ __forceinline__ double round3(double x) { return rint(x * 1000.0) / 1000.0; }
+
+// amg_test.py:69-78; -1 when either value is NaN (dropna() at :101).
+__device__ __forceinline__ int quadrant(double arousal, double valence) {
+    if (__builtin_isnan(arousal) || __builtin_isnan(valence)) return -1;
+    if (arousal >= 0.0 && valence >= 0.0) return 0;
+    if (arousal > 0.0 && valence < 0.0) return 1;
+    if (arousal <= 0.0 && valence <= 0.0) return 2;
+    return 3;  // arousal < 0 && valence > 0: the only case left for non-NaN input
+}
+
+__device__ __forceinline__ double bf16_to_f64(uint32_t h16) {
+    return (double)__uint_as_float(h16 << 16);
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// ---------------------------------------------------------------------------
+// Loads of one member's C class probabilities of one item, widened to f64.
+// VEC: C contiguous and 16-B (f32/f64) / 8-B (bf16) aligned -> vector loads.
+// ---------------------------------------------------------------------------
+template <int DT, int C, bool VEC>
+struct MemberLoad;
+
+template <int C>
+struct MemberLoad<kF32, C, true> {
+    static_assert(C % 4 == 0, "");
+    f32x4 v[C / 4];
+    __device__ __forceinline__ void load(const void* base, int64_t off, int64_t) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + off);
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) v[k] = __builtin_nontemporal_load(p + k);
+    }
+    __device__ __forceinline__ void add_to(double (&acc)[C]) const {
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) {
+            acc[4 * k + 0] += (double)v[k].x;
+            acc[4 * k + 1] += (double)v[k].y;
+            acc[4 * k + 2] += (double)v[k].z;
+            acc[4 * k + 3] += (double)v[k].w;
+        }
+    }
+};
+
+template <int C>
+struct MemberLoad<kF64, C, true> {
+    static_assert(C % 2 == 0, "");
+    f64x2 v[C / 2];
+    __device__ __forceinline__ void load(const void* base, int64_t off, int64_t) {
+        const f64x2* p = reinterpret_cast<const f64x2*>(static_cast<const double*>(base) + off);
+#pragma unroll
+        for (int k = 0; k < C / 2; ++k) v[k] = __builtin_nontemporal_load(p + k);
+    }
+    __device__ __forceinline__ void add_to(double (&acc)[C]) const {
+#pragma unroll
+        for (int k = 0; k < C / 2; ++k) {
+            acc[2 * k + 0] += v[k].x;
+            acc[2 * k + 1] += v[k].y;
+        }
+    }
+};
+
+template <int C>
+struct MemberLoad<kBF16, C, true> {
+    static_assert(C % 4 == 0, "");
+    u32x2 v[C / 4];
+    __device__ __forceinline__ void load(const void* base, int64_t off, int64_t) {
+        const u32x2* p = reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(base) + off);
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) v[k] = __builtin_nontemporal_load(p + k);
+    }
+    __device__ __forceinline__ void add_to(double (&acc)[C]) const {
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) {
+            acc[4 * k + 0] += bf16_to_f64(v[k].x & 0xffffu);
+            acc[4 * k + 1] += bf16_to_f64(v[k].x >> 16);
+            acc[4 * k + 2] += bf16_to_f64(v[k].y & 0xffffu);
+            acc[4 * k + 3] += bf16_to_f64(v[k].y >> 16);
+        }
+    }
+};
+
+// Scalar (any stride / alignment) variant.
+template <int DT, int C>
+struct MemberLoad<DT, C, false> {
+    double v[C];
+    __device__ __forceinline__ void load(const void* base, int64_t off, int64_t sC) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int64_t o = off + c * sC;
+            if constexpr (DT == kF32)
+                v[c] = (double)static_cast<const float*>(base)[o];
+            else if constexpr (DT == kF64)
+                v[c] = static_cast<const double*>(base)[o];
+            else
+                v[c] = bf16_to_f64(static_cast<const uint16_t*>(base)[o]);
+        }
+    }
+    __device__ __forceinline__ void add_to(double (&acc)[C]) const {
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] += v[c];
+    }
+};
+
+// Consensus mean of one item over M members, member-sequential (amg_test.py:441),
+// with up to UNR member loads in flight before the in-order adds.
+template <int DT, int C, bool VEC, int UNR>
+__device__ __forceinline__ void committee_mean(const void* p, int64_t item_off, int M, int64_t sM,
+                                               int64_t sC, double dM, double invM, bool pow2,
+                                               double (&mean)[C]) {
+    double acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = 0.0;  // np.add.reduce identity
+    int m = 0;
+    for (; m + UNR <= M; m += UNR) {
+        MemberLoad<DT, C, VEC> ld[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) ld[u].load(p, item_off + (int64_t)(m + u) * sM, sC);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) ld[u].add_to(acc);
+    }
+    for (; m < M; ++m) {
+        MemberLoad<DT, C, VEC> ld;
+        ld.load(p, item_off + (int64_t)m * sM, sC);
+        ld.add_to(acc);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) mean[c] = div_members(acc[c], dM, invM, pow2);
+}
+
+}  // namespace ce

@@ -1,0 +1,802 @@
+// ce_kernels.hip -- MI355X (gfx950) kernels and the C-ABI of include/ce.h.
+//
+// Kernels (DESIGN.md has the roofline of each):
+//   k_partial<Src>   score items (committee consensus entropy, an entropy
+//                    vector, or an hc table row) and keep a per-block top-q in
+//                    LDS; one pass over HBM, entropies never written back.
+//                    Replaces amg_test.py:441-445 / :451-452 / :479-480.
+//   k_finish         merge the blocks' (or ranks') candidate lists into the
+//                    final top-q; one block per segment (user / pool).
+//   k_entropy        per-item entropy to HBM (ce_committee_entropy).
+//   k_vote / k_va    hc frequency table + entropy from votes (amg_test.py:88-117).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdarg.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "../../include/ce.h"
+#include "ce_device.hpp"
+#include "ce_topq.hpp"
+#include "ce_wide.hpp"
+
+namespace ce {
+
+constexpr int kBS = 256;          // stage-1 block: 4 waves
+constexpr int kFinBS = 1024;      // stage-2 block: 16 waves
+constexpr int kMinRounds = 4;     // >= 4 rounds of kBS items per stage-1 block
+constexpr int kMaxBlocks = 1024;  // stage-1 blocks per pool (4 per CU on 256 CUs)
+
+// ---------------------------------------------------------------------------
+// Item sources.  key(i) returns the order key of global item i.
+// ---------------------------------------------------------------------------
+template <int DT, int C, bool VEC>
+struct CommitteeSrc {
+    const void* p;
+    int64_t sN, sM, sC;
+    int M;
+    double dM, invM;
+    bool pow2;
+    static constexpr int kC = C;
+    __device__ __forceinline__ void mean(int64_t i, double (&m)[C]) const {
+        committee_mean<DT, C, VEC, (DT == kF64 ? 4 : 8)>(p, i * sN, M, sM, sC, dM, invM, pow2, m);
+    }
+    __device__ __forceinline__ double entropy(int64_t i) const {
+        double m[C];
+        mean(i, m);
+        return entropy_row<C>(m);
+    }
+    __device__ __forceinline__ uint64_t key(int64_t i) const { return order_key(entropy(i)); }
+};
+
+struct ArraySrc {  // precomputed entropies
+    const double* e;
+    __device__ __forceinline__ uint64_t key(int64_t i) const { return order_key(e[i]); }
+};
+
+template <int C>
+struct TableSrc {  // hc frequency table rows [N_h, C] f64 (amg_test.py:451)
+    const double* t;
+    int64_t ld;
+    __device__ __forceinline__ uint64_t key(int64_t i) const {
+        double row[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) row[c] = t[i * ld + c];
+        return order_key(entropy_row<C>(row));
+    }
+};
+
+// Segment geometry: block b -> segment b / bpu, chunk b % bpu.
+struct Seg {
+    const int64_t* offsets;  // [U+1] device, or nullptr: one segment [0, N)
+    int64_t N;
+    int bpu;
+    int64_t base_idx;
+};
+
+__device__ __forceinline__ void seg_range(const Seg& sg, int64_t& s0, int64_t& lo, int64_t& hi) {
+    const int b = blockIdx.x;
+    const int u = b / sg.bpu, c = b % sg.bpu;
+    int64_t s1;
+    if (sg.offsets) {
+        s0 = sg.offsets[u];
+        s1 = sg.offsets[u + 1];
+    } else {
+        s0 = 0;
+        s1 = sg.N;
+    }
+    const int64_t len = s1 > s0 ? s1 - s0 : 0;
+    int64_t per = (len + sg.bpu - 1) / sg.bpu;
+    per = (per + kBS - 1) / kBS * kBS;
+    lo = s0 + (int64_t)c * per;
+    hi = lo + per < s1 ? lo + per : s1;
+    if (lo > hi) lo = hi;
+}
+
+// Write a finished top-q: either (key, idx) candidates into the workspace, or
+// the final (val, idx) outputs.  Slots past `cnt` are padding (idx -1).
+template <int CAP, bool FINAL>
+__device__ __forceinline__ void write_list(const TopQSmem<CAP>& s, int cnt, int q, uint64_t* wkey,
+                                           int64_t* widx, double* oval, int64_t* oidx) {
+    for (int r = threadIdx.x; r < q; r += blockDim.x) {
+        const bool ok = r < cnt;
+        if constexpr (FINAL) {
+            oval[r] = ok ? key_to_val(s.key[r]) : __longlong_as_double(0x7ff8000000000000ll);
+            oidx[r] = ok ? s.idx[r] : -1;
+        } else {
+            wkey[r] = ok ? s.key[r] : 0ull;
+            widx[r] = ok ? s.idx[r] : -1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1: score + per-block top-q.  One item per thread per round.
+// ---------------------------------------------------------------------------
+template <class Src, int CAP, bool FINAL>
+__global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, uint64_t* __restrict__ wkey,
+                                                 int64_t* __restrict__ widx, double* __restrict__ oval,
+                                                 int64_t* __restrict__ oidx) {
+    __shared__ TopQSmem<CAP> sm;
+    TopQ<CAP, kBS> tq(sm);
+    tq.init();
+    int64_t s0, lo, hi;
+    seg_range(sg, s0, lo, hi);
+    const int64_t rel = sg.base_idx - s0;
+    for (int64_t i0 = lo; i0 < hi; i0 += kBS) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool valid = i < hi;
+        uint64_t k = 0;
+        if (valid) k = src.key(i);
+        tq.offer(k, i + rel, valid);
+        tq.end_round(q, kBS);
+    }
+    const int cnt = tq.finish(q);
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    write_list<CAP, FINAL>(sm, cnt, q, wkey + slot, widx + slot, oval + (FINAL ? slot : 0),
+                           oidx + (FINAL ? slot : 0));
+}
+
+// Wide-class variant: a wave scores 64 consecutive items (one per lane slot),
+// so a block round is still 256 candidates.
+template <int DT, int KMAX, int CAP, bool FINAL>
+__global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q,
+                                                      uint64_t* __restrict__ wkey, int64_t* __restrict__ widx,
+                                                      double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    __shared__ TopQSmem<CAP> sm;
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    TopQ<CAP, kBS> tq(sm);
+    tq.init();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    int64_t s0, lo, hi;
+    seg_range(sg, s0, lo, hi);
+    const int64_t rel = sg.base_idx - s0;
+    for (int64_t i0 = lo; i0 < hi; i0 += kBS) {
+        uint64_t mykey = 0;
+        const int64_t wbase = i0 + 64 * w;
+        for (int j = 0; j < 64; ++j) {
+            const int64_t it = wbase + j;
+            if (it >= hi) break;  // wave-uniform
+            const double h = wave_item_entropy<DT, KMAX>(a.p, it * a.sN, a.M, a.C, a.sM, a.sC, a.dM, a.invM,
+                                                         a.pow2, pl, row, scratch, nullptr);
+            if (lane == j) mykey = order_key(h);
+        }
+        const int64_t i = i0 + threadIdx.x;
+        tq.offer(mykey, i + rel, i < hi);
+        tq.end_round(q, kBS);
+    }
+    const int cnt = tq.finish(q);
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    write_list<CAP, FINAL>(sm, cnt, q, wkey + slot, widx + slot, oval + (FINAL ? slot : 0),
+                           oidx + (FINAL ? slot : 0));
+}
+
+// ---------------------------------------------------------------------------
+// Stage 2: merge `nl` lists of q slots (per segment = blockIdx.x) into top-q.
+// A list's worst entry bounds the answer from below: with T = the best of the
+// full lists' worst entries, at least q candidates are >= T, so only
+// candidates >= T can be selected -- the filter is exact and usually leaves
+// ~q survivors.
+// ---------------------------------------------------------------------------
+template <bool FROM_VALS>
+struct ListSrc {
+    const uint64_t* key;
+    const double* val;
+    const int64_t* idx;
+    __device__ __forceinline__ void get(int64_t j, uint64_t& k, int64_t& i) const {
+        i = idx[j];
+        if constexpr (FROM_VALS)
+            k = order_key(val[j]);
+        else
+            k = key[j];
+    }
+};
+
+__device__ __forceinline__ void wave_best(uint64_t& k, int64_t& i) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t k2 = __shfl_xor(k, off);
+        const int64_t i2 = __shfl_xor(i, off);
+        if (better(k2, i2, k, i)) {
+            k = k2;
+            i = i2;
+        }
+    }
+}
+
+template <bool FROM_VALS, int CAP, int BS, int IPT>
+__global__ __launch_bounds__(BS) void k_finish(ListSrc<FROM_VALS> src, int nl, int q,
+                                               double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    __shared__ TopQSmem<CAP> sm;
+    __shared__ uint64_t wk[BS / 64];
+    __shared__ int64_t wi[BS / 64];
+    const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
+    // 1. T = best over full lists of the list's worst entry.
+    uint64_t tk = 0;
+    int64_t ti = INT64_MAX;  // "nothing": worse than any real candidate
+    for (int g = threadIdx.x; g < nl; g += BS) {
+        uint64_t wkk = ~0ull;
+        int64_t wii = -1;
+        bool full = true;
+        for (int r = 0; r < q; ++r) {
+            uint64_t k;
+            int64_t i;
+            src.get(seg0 + (int64_t)g * q + r, k, i);
+            if (i < 0) {
+                full = false;
+                break;
+            }
+            if (better(wkk, wii, k, i)) {
+                wkk = k;
+                wii = i;
+            }
+        }
+        if (full && better(wkk, wii, tk, ti)) {
+            tk = wkk;
+            ti = wii;
+        }
+    }
+    wave_best(tk, ti);
+    if (lane_id() == 0) {
+        wk[threadIdx.x >> 6] = tk;
+        wi[threadIdx.x >> 6] = ti;
+    }
+    __syncthreads();
+    tk = wk[0];
+    ti = wi[0];
+    for (int w = 1; w < BS / 64; ++w)
+        if (better(wk[w], wi[w], tk, ti)) {
+            tk = wk[w];
+            ti = wi[w];
+        }
+    // admit candidates >= T: strictly better than (T.key, T.idx + 1)
+    TopQ<CAP, BS> tq(sm);
+    tq.init(tk, ti == INT64_MAX ? INT64_MAX : ti + 1);
+    // 2. filter all candidates, IPT per thread in flight
+    const int64_t L = (int64_t)nl * q;
+    for (int64_t b0 = 0; b0 < L; b0 += (int64_t)BS * IPT) {
+        uint64_t k[IPT];
+        int64_t id[IPT];
+#pragma unroll
+        for (int u = 0; u < IPT; ++u) {
+            const int64_t j = b0 + (int64_t)u * BS + threadIdx.x;
+            k[u] = 0;
+            id[u] = -1;
+            if (j < L) src.get(seg0 + j, k[u], id[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < IPT; ++u) {
+            tq.offer(k[u], id[u], id[u] >= 0);
+            tq.end_round(q, BS);
+        }
+    }
+    const int cnt = tq.finish(q);
+    write_list<CAP, true>(sm, cnt, q, nullptr, nullptr, oval + (int64_t)blockIdx.x * q,
+                          oidx + (int64_t)blockIdx.x * q);
+}
+
+// ---------------------------------------------------------------------------
+// Per-item entropy to HBM.
+// ---------------------------------------------------------------------------
+template <class Src>
+__global__ __launch_bounds__(kBS) void k_entropy(Src src, int64_t N, double* __restrict__ mean_out,
+                                                 double* __restrict__ ent) {
+    constexpr int C = Src::kC;
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBS) {
+        double mean[C];
+        src.mean(i, mean);
+        if (mean_out)
+#pragma unroll
+            for (int c = 0; c < C; ++c) mean_out[i * C + c] = mean[c];
+        ent[i] = entropy_row<C>(mean);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// hc tables: one wave per row (amg_test.py:109-117).
+// ---------------------------------------------------------------------------
+template <int C>
+__device__ __forceinline__ void finish_counts(int (&cnt)[C], int64_t n_row, double* freq_out,
+                                              double* ent) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cnt[c] += __shfl_xor(cnt[c], off);
+    if (lane_id() == 0) {
+        int n = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) n += cnt[c];
+        double f[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) f[c] = round3((double)cnt[c] / (double)n);
+        if (freq_out)
+#pragma unroll
+            for (int c = 0; c < C; ++c) freq_out[n_row * C + c] = f[c];
+        ent[n_row] = entropy_row<C>(f);
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(kBS) void k_vote(const int8_t* __restrict__ votes, int64_t N, int A, int64_t ld,
+                                              double* __restrict__ freq, double* __restrict__ ent) {
+    const int lane = lane_id();
+    for (int64_t n = (int64_t)blockIdx.x * (kBS / 64) + (threadIdx.x >> 6); n < N;
+         n += (int64_t)gridDim.x * (kBS / 64)) {
+        int cnt[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) cnt[c] = 0;
+        const int8_t* row = votes + n * ld;
+        for (int a = lane; a < A; a += 64) {
+            const int v = row[a];
+#pragma unroll
+            for (int c = 0; c < C; ++c) cnt[c] += (v == c);
+        }
+        finish_counts<C>(cnt, n, freq, ent);
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_va(const double* __restrict__ va, int64_t N, int A,
+                                            double* __restrict__ freq, double* __restrict__ ent) {
+    const int lane = lane_id();
+    for (int64_t n = (int64_t)blockIdx.x * (kBS / 64) + (threadIdx.x >> 6); n < N;
+         n += (int64_t)gridDim.x * (kBS / 64)) {
+        int cnt[4] = {0, 0, 0, 0};
+        const double2* row = reinterpret_cast<const double2*>(va) + n * A;
+        for (int a = lane; a < A; a += 64) {
+            const double2 x = row[a];  // (valence, arousal)
+            const int qd = quadrant(x.y, x.x);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) cnt[c] += (qd == c);
+        }
+        finish_counts<4>(cnt, n, freq, ent);
+    }
+}
+
+}  // namespace ce
+
+// ===========================================================================
+// Host side: argument checks, geometry, dispatch, C-ABI.
+// ===========================================================================
+using namespace ce;
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+static int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(CE_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+    g_err[0] = 0;
+    return CE_OK;
+}
+
+extern "C" const char* ce_last_error(void) { return g_err; }
+extern "C" const char* ce_version(void) { return "ce_amd 0.1 gfx950"; }
+
+static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// stage-1 blocks for a pool of n items (host arithmetic only: ws sizing and
+// launches agree by construction)
+static int pool_blocks(int64_t n) {
+    int64_t g = cdiv(n, (int64_t)kBS * kMinRounds);
+    if (g < 1) g = 1;
+    if (g > kMaxBlocks) g = kMaxBlocks;
+    return (int)g;
+}
+
+static size_t lists_bytes(int64_t nlists, int q) { return (size_t)nlists * (size_t)q * 16u + 256u; }
+
+struct WsLists {
+    uint64_t* key;
+    int64_t* idx;
+};
+static WsLists carve(void* ws, int64_t nlists, int q) {
+    uintptr_t p = ((uintptr_t)ws + 255) & ~(uintptr_t)255;
+    WsLists w;
+    w.key = reinterpret_cast<uint64_t*>(p);
+    w.idx = reinterpret_cast<int64_t*>(p + (size_t)nlists * q * 8u);
+    return w;
+}
+
+static int check_q(int q) {
+    if (q < 1 || q > CE_MAX_Q) return fail(CE_EINVAL, "q=%d outside [1, %d]", q, CE_MAX_Q);
+    return CE_OK;
+}
+
+template <class Src>
+static void launch_partial(const Src& src, const Seg& sg, int grid, int q, WsLists w, double* oval,
+                           int64_t* oidx, bool final_out, hipStream_t st) {
+    if (q <= 256) {
+        if (final_out)
+            hipLaunchKernelGGL((k_partial<Src, 1024, true>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
+                               w.idx, oval, oidx);
+        else
+            hipLaunchKernelGGL((k_partial<Src, 1024, false>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
+                               w.idx, oval, oidx);
+    } else {
+        if (final_out)
+            hipLaunchKernelGGL((k_partial<Src, 4096, true>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
+                               w.idx, oval, oidx);
+        else
+            hipLaunchKernelGGL((k_partial<Src, 4096, false>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
+                               w.idx, oval, oidx);
+    }
+}
+
+template <bool FROM_VALS>
+static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, double* oval, int64_t* oidx,
+                          hipStream_t st) {
+    const int64_t L = (int64_t)nl * q;
+    if (L <= 256 && q <= 128)
+        hipLaunchKernelGGL((k_finish<FROM_VALS, 512, 256, 1>), dim3(segments), dim3(256), 0, st, src, nl, q,
+                           oval, oidx);
+    else
+        hipLaunchKernelGGL((k_finish<FROM_VALS, 4096, kFinBS, 8>), dim3(segments), dim3(kFinBS), 0, st, src,
+                           nl, q, oval, oidx);
+}
+
+// ---- committee dispatch ----------------------------------------------------
+struct CommArgs {
+    const void* p;
+    int dt;
+    int64_t N;
+    int M, C;
+    int64_t sN, sM, sC;
+};
+
+static int check_comm(const CommArgs& a) {
+    if (!a.p && a.N > 0) return fail(CE_EINVAL, "null committee pointer");
+    if (a.N < 0 || a.M < 1 || a.C < 1) return fail(CE_EINVAL, "bad shape N=%lld M=%d C=%d", (long long)a.N, a.M, a.C);
+    if (a.dt < 0 || a.dt > 2) return fail(CE_EINVAL, "bad dtype %d", a.dt);
+    return CE_OK;
+}
+
+static int elem_bytes(int dt) { return dt == kF64 ? 8 : (dt == kF32 ? 4 : 2); }
+
+static bool vec_ok(const CommArgs& a, int C) {
+    if (a.sC != 1) return false;
+    const int eb = elem_bytes(a.dt);
+    const int vb = a.dt == kBF16 ? 8 : 16;  // bytes per vector load
+    if (a.dt == kF64 ? (C % 2) : (C % 4)) return false;
+    if ((uintptr_t)a.p % vb) return false;
+    if ((a.sN * eb) % vb || (a.sM * eb) % vb) return false;
+    return true;
+}
+
+template <int DT, int C, bool VEC>
+static CommitteeSrc<DT, C, VEC> make_src(const CommArgs& a) {
+    CommitteeSrc<DT, C, VEC> s;
+    s.p = a.p;
+    s.sN = a.sN;
+    s.sM = a.sM;
+    s.sC = a.sC;
+    s.M = a.M;
+    s.dM = (double)a.M;
+    s.invM = 1.0 / (double)a.M;
+    s.pow2 = (a.M & (a.M - 1)) == 0;
+    return s;
+}
+
+// Calls f(src) with the CommitteeSrc instantiation matching (dtype, C, vec).
+template <class F>
+static int with_committee(const CommArgs& a, F&& f) {
+#define CE_CASE(DT_, C_)                                       \
+    if (a.dt == DT_ && a.C == C_) {                            \
+        if (vec_ok(a, C_)) f(make_src<DT_, C_, true>(a));      \
+        else f(make_src<DT_, C_, false>(a));                   \
+        return CE_OK;                                          \
+    }
+    CE_CASE(kF32, 4) CE_CASE(kF64, 4) CE_CASE(kBF16, 4)
+    CE_CASE(kF32, 8) CE_CASE(kF64, 8) CE_CASE(kBF16, 8)
+    CE_CASE(kF64, 2)
+#undef CE_CASE
+#define CE_CASE_S(DT_, C_)                                     \
+    if (a.dt == DT_ && a.C == C_) {                            \
+        f(make_src<DT_, C_, false>(a));                        \
+        return CE_OK;                                          \
+    }
+    CE_CASE_S(kF32, 2) CE_CASE_S(kBF16, 2)
+    CE_CASE_S(kF32, 3) CE_CASE_S(kF64, 3) CE_CASE_S(kBF16, 3)
+#undef CE_CASE_S
+    return CE_EUNSUPPORTED;
+}
+
+// ---- wide-class dispatch (C not in the register-path set) -------------------
+static WideArgs wide_args(const CommArgs& a) {
+    WideArgs w{a.p, a.N, a.M, a.C, a.sN, a.sM, a.sC, (double)a.M, 1.0 / (double)a.M, (a.M & (a.M - 1)) == 0};
+    return w;
+}
+static size_t wide_lds_bytes(int C) { return (size_t)4 * wide_lds_doubles(C) * sizeof(double); }
+
+// f(dt_tag, kmax_tag) with compile-time DT / KMAX
+template <class F>
+static int with_wide(const CommArgs& a, F&& f) {
+    if (a.C > kWideMaxC) return CE_EUNSUPPORTED;
+    const int k = (a.C + 63) / 64;
+#define CE_W(DT_)                                                                   \
+    if (a.dt == DT_) {                                                              \
+        if (k <= 1) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 1>());        \
+        else if (k <= 2) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 2>());   \
+        else if (k <= 4) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 4>());   \
+        else if (k <= 8) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 8>());   \
+        else if (k <= 16) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 16>()); \
+        else f(std::integral_constant<int, DT_>(), std::integral_constant<int, 32>());              \
+        return CE_OK;                                                               \
+    }
+    CE_W(kF32) CE_W(kF64) CE_W(kBF16)
+#undef CE_W
+    return CE_EUNSUPPORTED;
+}
+
+static void launch_partial_wide(const CommArgs& a, const Seg& sg, int grid, int q, WsLists w, double* oval,
+                                int64_t* oidx, bool fin, hipStream_t st) {
+    const WideArgs wa = wide_args(a);
+    const PwPlan pl = pw_plan(a.C);
+    const size_t lds = wide_lds_bytes(a.C);
+    with_wide(a, [&](auto dt, auto km) {
+        constexpr int DT = decltype(dt)::value, KM = decltype(km)::value;
+        if (q <= 256) {
+            if (fin)
+                hipLaunchKernelGGL((k_partial_wide<DT, KM, 1024, true>), dim3(grid), dim3(kBS), lds, st, wa, pl, sg,
+                                   q, w.key, w.idx, oval, oidx);
+            else
+                hipLaunchKernelGGL((k_partial_wide<DT, KM, 1024, false>), dim3(grid), dim3(kBS), lds, st, wa, pl,
+                                   sg, q, w.key, w.idx, oval, oidx);
+        } else {
+            if (fin)
+                hipLaunchKernelGGL((k_partial_wide<DT, KM, 4096, true>), dim3(grid), dim3(kBS), lds, st, wa, pl, sg,
+                                   q, w.key, w.idx, oval, oidx);
+            else
+                hipLaunchKernelGGL((k_partial_wide<DT, KM, 4096, false>), dim3(grid), dim3(kBS), lds, st, wa, pl,
+                                   sg, q, w.key, w.idx, oval, oidx);
+        }
+    });
+}
+
+// Committee stage 1 for any supported shape: register path or wide path.
+static int committee_partial(const CommArgs& a, const Seg& sg, int grid, int q, WsLists w, double* oval,
+                             int64_t* oidx, bool fin, hipStream_t st) {
+    int rc = with_committee(a, [&](auto src) { launch_partial(src, sg, grid, q, w, oval, oidx, fin, st); });
+    if (rc != CE_EUNSUPPORTED) return rc;
+    if (a.C > kWideMaxC) return CE_EUNSUPPORTED;
+    launch_partial_wide(a, sg, grid, q, w, oval, oidx, fin, st);
+    return CE_OK;
+}
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+static int dispatch_err(int rc, const CommArgs& a) {
+    if (rc == CE_EUNSUPPORTED)
+        return fail(CE_EUNSUPPORTED, "committee shape C=%d dtype=%d has no kernel in this build", a.C, a.dt);
+    return rc;
+}
+
+extern "C" int ce_committee_entropy(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                                    int64_t sM, int64_t sC, double* mean_or_null, double* ent,
+                                    ce_stream_t stream) {
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int rc = check_comm(a);
+    if (rc) return rc;
+    if (!ent) return fail(CE_EINVAL, "null ent");
+    if (N == 0) return CE_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int grid = (int)std::min<int64_t>(cdiv(N, kBS), 4096);
+    rc = with_committee(a, [&](auto src) {
+        hipLaunchKernelGGL((k_entropy<decltype(src)>), dim3(grid), dim3(kBS), 0, st, src, N, mean_or_null, ent);
+    });
+    if (rc == CE_EUNSUPPORTED) {
+        const WideArgs wa = wide_args(a);
+        const PwPlan pl = pw_plan(C);
+        const size_t lds = wide_lds_bytes(C);
+        const int wgrid = (int)std::min<int64_t>(cdiv(N, 4), 8192);
+        rc = with_wide(a, [&](auto dt, auto km) {
+            hipLaunchKernelGGL((k_wide_entropy<decltype(dt)::value, decltype(km)::value>), dim3(wgrid), dim3(256),
+                               lds, st, wa, pl, mean_or_null, ent);
+        });
+    }
+    if (rc) return dispatch_err(rc, a);
+    return check_launch("ce_committee_entropy");
+}
+
+extern "C" int ce_vote_entropy(const int8_t* votes, int64_t N, int32_t A, int32_t C, int64_t ld,
+                               double* freq_or_null, double* ent, ce_stream_t stream) {
+    if (N < 0 || A < 0 || ld < A) return fail(CE_EINVAL, "bad vote matrix N=%lld A=%d ld=%lld", (long long)N, A, (long long)ld);
+    if (!ent || (N > 0 && !votes)) return fail(CE_EINVAL, "null pointer");
+    if (N == 0) return CE_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int grid = (int)std::min<int64_t>(cdiv(N, kBS / 64), 8192);
+    switch (C) {
+#define CE_V(CC) case CC: hipLaunchKernelGGL((k_vote<CC>), dim3(grid), dim3(kBS), 0, st, votes, N, A, ld, freq_or_null, ent); break;
+        CE_V(1) CE_V(2) CE_V(3) CE_V(4) CE_V(5) CE_V(6) CE_V(7) CE_V(8)
+#undef CE_V
+        default: return fail(CE_EUNSUPPORTED, "vote classes C=%d outside [1, 8]", C);
+    }
+    return check_launch("ce_vote_entropy");
+}
+
+extern "C" int ce_va_entropy(const double* va, int64_t N, int32_t A, double* freq_or_null, double* ent,
+                             ce_stream_t stream) {
+    if (N < 0 || A < 0) return fail(CE_EINVAL, "bad annotation array");
+    if (!ent || (N > 0 && !va)) return fail(CE_EINVAL, "null pointer");
+    if ((uintptr_t)va % 16) return fail(CE_EINVAL, "va must be 16-byte aligned");
+    if (N == 0) return CE_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int grid = (int)std::min<int64_t>(cdiv(N, kBS / 64), 8192);
+    hipLaunchKernelGGL(k_va, dim3(grid), dim3(kBS), 0, st, va, N, A, freq_or_null, ent);
+    return check_launch("ce_va_entropy");
+}
+
+// ---- top-q of an entropy vector -------------------------------------------
+extern "C" size_t ce_topq_workspace_bytes(int64_t N, int32_t q) {
+    return lists_bytes(pool_blocks(N), q < 1 ? 1 : q);
+}
+
+static int finish_lists(WsLists w, int segments, int nl, int q, double* val_out, int64_t* idx_out,
+                        hipStream_t st) {
+    ListSrc<false> ls{w.key, nullptr, w.idx};
+    launch_finish(ls, segments, nl, q, val_out, idx_out, st);
+    return CE_OK;
+}
+
+extern "C" int ce_topq(const double* ent, int64_t N, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes,
+                       double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (N < 0 || !val_out || !idx_out || (N > 0 && !ent)) return fail(CE_EINVAL, "bad topq arguments");
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, G, q);
+    Seg sg{nullptr, N, G, base_idx};
+    launch_partial(ArraySrc{ent}, sg, G, q, w, val_out, idx_out, G == 1, st);
+    if (G > 1) finish_lists(w, 1, G, q, val_out, idx_out, st);
+    return check_launch("ce_topq");
+}
+
+extern "C" int ce_topq_merge(const double* vals, const int64_t* idx, int32_t nlists, int32_t q, double* val_out,
+                             int64_t* idx_out, ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (nlists < 1 || !vals || !idx || !val_out || !idx_out) return fail(CE_EINVAL, "bad merge arguments");
+    ListSrc<true> ls{nullptr, vals, idx};
+    launch_finish(ls, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
+    return check_launch("ce_topq_merge");
+}
+
+// ---- fused mc ----------------------------------------------------------------
+extern "C" size_t ce_select_mc_workspace_bytes(int64_t N, int32_t q) { return ce_topq_workspace_bytes(N, q); }
+
+static int mc_partial(const CommArgs& a, int q, int64_t base_idx, void* ws, size_t ws_bytes, double* val_out,
+                      int64_t* idx_out, bool allow_final, int* G_out, hipStream_t st) {
+    int rc = check_comm(a);
+    if (rc) return rc;
+    rc = check_q(q);
+    if (rc) return rc;
+    const int G = pool_blocks(a.N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    WsLists w = carve(ws, G, q);
+    Seg sg{nullptr, a.N, G, base_idx};
+    const bool fin = allow_final && G == 1;
+    rc = committee_partial(a, sg, G, q, w, val_out, idx_out, fin, st);
+    if (rc) return dispatch_err(rc, a);
+    *G_out = G;
+    return CE_OK;
+}
+
+extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                            int64_t sC, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes, double* val_out,
+                            int64_t* idx_out, ce_stream_t stream) {
+    if (!val_out || !idx_out) return fail(CE_EINVAL, "null output");
+    hipStream_t st = (hipStream_t)stream;
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int G = 0;
+    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, st);
+    if (rc) return rc;
+    if (G > 1) finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
+    return check_launch("ce_select_mc");
+}
+
+extern "C" int ce_select_mc_partial(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                                    int64_t sM, int64_t sC, int32_t q, int64_t base_idx, void* ws,
+                                    size_t ws_bytes, ce_stream_t stream) {
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int G = 0;
+    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &G, (hipStream_t)stream);
+    if (rc) return rc;
+    return check_launch("ce_select_mc_partial");
+}
+
+extern "C" int ce_select_finish(int64_t N, int32_t q, void* ws, size_t ws_bytes, double* val_out, int64_t* idx_out,
+                                ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (N < 0 || !val_out || !idx_out) return fail(CE_EINVAL, "bad finish arguments");
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, (hipStream_t)stream);
+    return check_launch("ce_select_finish");
+}
+
+// ---- fused mix ---------------------------------------------------------------
+extern "C" size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t q) {
+    return lists_bytes((int64_t)pool_blocks(N) + pool_blocks(N_h), q < 1 ? 1 : q);
+}
+
+extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                             int64_t sC, const double* hc, int64_t N_h, int64_t ld_hc, int32_t q, void* ws,
+                             size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int rc = check_comm(a);
+    if (rc) return rc;
+    rc = check_q(q);
+    if (rc) return rc;
+    if (N_h < 0 || (N_h > 0 && (!hc || ld_hc < C)) || !val_out || !idx_out)
+        return fail(CE_EINVAL, "bad hc table / outputs");
+    const int G1 = pool_blocks(N), G2 = pool_blocks(N_h);
+    if (!ws || ws_bytes < lists_bytes((int64_t)G1 + G2, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, (int64_t)G1 + G2, q);
+    Seg s1{nullptr, N, G1, 0};
+    rc = committee_partial(a, s1, G1, q, w, nullptr, nullptr, false, st);
+    if (rc) return dispatch_err(rc, a);
+    WsLists w2{w.key + (size_t)G1 * q, w.idx + (size_t)G1 * q};
+    Seg s2{nullptr, N_h, G2, N};
+    switch (C) {
+#define CE_T(CC) case CC: launch_partial(TableSrc<CC>{hc, ld_hc}, s2, G2, q, w2, nullptr, nullptr, false, st); break;
+        CE_T(2) CE_T(3) CE_T(4) CE_T(8)
+#undef CE_T
+        default: return fail(CE_EUNSUPPORTED, "mix with C=%d has no kernel in this build", C);
+    }
+    finish_lists(w, 1, G1 + G2, q, val_out, idx_out, st);
+    return check_launch("ce_select_mix");
+}
+
+// ---- batched users -------------------------------------------------------------
+static int batched_bpu(int64_t total, int U) {
+    if (U < 1) return 1;
+    const int64_t avg = cdiv(total, U);
+    int64_t bpu = cdiv(avg, (int64_t)kBS * kMinRounds);
+    const int64_t cap = std::max<int64_t>(1, 2048 / U);
+    bpu = std::max<int64_t>(1, std::min(bpu, cap));
+    return (int)bpu;
+}
+
+extern "C" size_t ce_select_batched_workspace_bytes(int64_t total_items, int32_t U, int32_t q) {
+    if (U < 1) U = 1;
+    return lists_bytes((int64_t)batched_bpu(total_items, U) * U, q < 1 ? 1 : q);
+}
+
+extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items, int32_t M, int32_t C, int64_t sN,
+                                 int64_t sM, int64_t sC, const int64_t* offsets, int32_t U, int32_t q, void* ws,
+                                 size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    CommArgs a{p, (int)dt, total_items, M, C, sN, sM, sC};
+    int rc = check_comm(a);
+    if (rc) return rc;
+    rc = check_q(q);
+    if (rc) return rc;
+    if (U < 1 || !offsets || !val_out || !idx_out) return fail(CE_EINVAL, "bad batched arguments");
+    const int bpu = batched_bpu(total_items, U);
+    const int64_t nl = (int64_t)bpu * U;
+    if (!ws || ws_bytes < lists_bytes(nl, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, nl, q);
+    Seg sg{offsets, total_items, bpu, 0};
+    const bool fin = bpu == 1;
+    rc = committee_partial(a, sg, (int)nl, q, w, val_out, idx_out, fin, st);
+    if (rc) return dispatch_err(rc, a);
+    if (!fin) finish_lists(w, U, bpu, q, val_out, idx_out, st);
+    return check_launch("ce_select_batched");
+}

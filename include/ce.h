@@ -1,0 +1,153 @@
+/*
+ * ce.h -- C-ABI of the MI355X consensus-entropy query-selection engine (libce_amd.so).
+ *
+ * The reference (juansgomez87/consensus-entropy) has no plugin/FFI interface: the
+ * selection path is ~60 lines of NumPy/SciPy inline in AMG_Tester.run
+ * (amg_test.py:425-489).  This header defines the drop-in seam at exactly that
+ * place; each entry point names the reference lines it replaces.  The Python
+ * mirror of the reference interface (consensus-entropy_amd/ce_amd) binds it with
+ * ctypes; INTEGRATION.md shows the binding a maintainer of the reference adds.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is caller-owned DEVICE memory unless stated otherwise;
+ *   - every call is stream-ordered on `stream` (a hipStream_t; NULL = legacy
+ *     default stream) and asynchronous: nothing is read back to the host;
+ *   - nothing allocates: scratch comes from the caller's `ws`, sized by the
+ *     matching *_workspace_bytes() function (pure host arithmetic);
+ *   - return 0 (CE_OK) or a negative CE_E* code; ce_last_error() gives a
+ *     thread-local message.  Nothing throws across the ABI;
+ *   - strides are in ELEMENTS.  Element (n, m, c) of a committee tensor lives at
+ *     p[n*sN + m*sM + c*sC]: the reference's member-major stack np.array(pred_prob)
+ *     ([M,N,C], amg_test.py:441) is sN=C, sM=N*C, sC=1; the item-major [N,M,C]
+ *     tensor is sN=M*C, sM=C, sC=1;
+ *   - arithmetic contract (BASELINE.json north_star): inputs are loaded as
+ *     f32/f64/bf16 and every sum, mean, normalisation and entropy is computed in
+ *     f64 in the reference's order (member-sequential mean, numpy pairwise row
+ *     sums, scipy.special.entr);
+ *   - selection order: NaN entropies first, then entropy descending, then lowest
+ *     index (the reference's argsort()[::-1] with its unspecified tie order
+ *     tightened to lowest-index-first; -0.0 == +0.0).  Selected outputs are q
+ *     slots, best first; slots beyond the number of candidates hold idx = -1 and
+ *     val = NaN.
+ */
+#ifndef CE_AMD_CE_H
+#define CE_AMD_CE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *ce_stream_t; /* hipStream_t */
+
+typedef enum { CE_F32 = 0, CE_F64 = 1, CE_BF16 = 2 } ce_dtype;
+
+enum {
+    CE_OK = 0,
+    CE_EINVAL = -1,       /* bad argument (shape, q, stride, null pointer) */
+    CE_EWORKSPACE = -2,   /* ws too small */
+    CE_ELAUNCH = -3,      /* HIP runtime error on launch */
+    CE_EUNSUPPORTED = -4  /* shape outside what this build implements */
+};
+
+#define CE_MAX_Q 2048
+
+const char *ce_last_error(void);
+const char *ce_version(void);
+
+/*
+ * Per-item committee consensus entropy -- replaces amg_test.py:441 + :443:
+ *   consensus_prob = np.mean(np.array(pred_prob), axis=0)
+ *   ent = scipy.stats.entropy(consensus_prob, axis=1)
+ * p: [N items x M members x C classes] via strides; ent: [N] f64 out.
+ * mean_or_null: optional [N, C] f64 out (the consensus_prob matrix).
+ */
+int ce_committee_entropy(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                         int64_t sM, int64_t sC, double *mean_or_null, double *ent,
+                         ce_stream_t stream);
+
+/*
+ * Human-consensus table -- replaces amg_test.py:109-117 (+ :451's entropy):
+ *   per row, count votes per class (votes[n*ld + a] in [0, C) is a vote, any
+ *   other value e.g. -1 is missing), freq = np.round(count / n_votes, 3),
+ *   ent = scipy.stats.entropy(freq).  A row with no vote gives NaN.
+ * votes: [N, A] int8 with row stride ld (bytes).  freq_or_null: [N, C] f64 out.
+ * C in [1, 8].
+ */
+int ce_vote_entropy(const int8_t *votes, int64_t N, int32_t A, int32_t C, int64_t ld,
+                    double *freq_or_null, double *ent, ce_stream_t stream);
+
+/*
+ * Same as ce_vote_entropy from the raw AMG1608 annotation array
+ * (amg_test.py:88-106): va[(n*A + a)*2 + 0] = valence, [.. + 1] = arousal, f64,
+ * NaN = missing (dropped as dropna() at :101); quadrant rule of :69-78; C = 4.
+ */
+int ce_va_entropy(const double *va, int64_t N, int32_t A, double *freq_or_null, double *ent,
+                  ce_stream_t stream);
+
+/*
+ * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]
+ * (amg_test.py:445, :452, :480).  Positions are reported as base_idx + i.
+ * val_out: [q] f64, idx_out: [q] int64.
+ */
+size_t ce_topq_workspace_bytes(int64_t N, int32_t q);
+int ce_topq(const double *ent, int64_t N, int32_t q, int64_t base_idx, void *ws, size_t ws_bytes,
+            double *val_out, int64_t *idx_out, ce_stream_t stream);
+
+/*
+ * Merge of nlists candidate lists of q slots each (vals/idx: [nlists*q], every
+ * list best-first as the ce_* outputs are; idx < 0 = empty slot) into the
+ * global top-q.  Used after the RCCL all-gather of per-GPU top-q lists.
+ */
+int ce_topq_merge(const double *vals, const int64_t *idx, int32_t nlists, int32_t q,
+                  double *val_out, int64_t *idx_out, ce_stream_t stream);
+
+/*
+ * Fused mc selection -- replaces amg_test.py:441-445 in one pass over the
+ * committee tensor (entropies never reach HBM): scores each item and keeps a
+ * per-block top-q in LDS, then merges the blocks' candidates.
+ * ce_select_mc_partial + ce_topq_merge_ws are the same two stages exposed
+ * separately (the multi-GPU driver and the bench time them apart).
+ */
+size_t ce_select_mc_workspace_bytes(int64_t N, int32_t q);
+int ce_select_mc(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                 int64_t sM, int64_t sC, int32_t q, int64_t base_idx, void *ws, size_t ws_bytes,
+                 double *val_out, int64_t *idx_out, ce_stream_t stream);
+int ce_select_mc_partial(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                         int64_t sM, int64_t sC, int32_t q, int64_t base_idx, void *ws,
+                         size_t ws_bytes, ce_stream_t stream);
+/* Stage 2 of ce_select_mc / ce_select_mix / ce_topq on a filled workspace. */
+int ce_select_finish(int64_t N, int32_t q, void *ws, size_t ws_bytes, double *val_out,
+                     int64_t *idx_out, ce_stream_t stream);
+
+/*
+ * Fused mix selection -- replaces amg_test.py:473-480: the ROW stack
+ * [mc consensus (N rows); hc table (N_h rows)], entropy, top-q over the union.
+ * Positions in [0, N) are committee items, [N, N + N_h) hc rows.
+ * hc: [N_h, C] f64 with row stride ld_hc (elements).
+ */
+size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t q);
+int ce_select_mix(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                  int64_t sM, int64_t sC, const double *hc, int64_t N_h, int64_t ld_hc, int32_t q,
+                  void *ws, size_t ws_bytes, double *val_out, int64_t *idx_out,
+                  ce_stream_t stream);
+
+/*
+ * Batched personalization -- replaces the per-user loop (amg_test.py:345) around
+ * :441-445: U independent pools in one launch.  User u owns items
+ * [offsets[u], offsets[u+1]) of the committee tensor (offsets: [U+1] int64,
+ * DEVICE memory; total_items = offsets[U] is passed for workspace sizing).
+ * Output slots [u*q, (u+1)*q); positions are user-local (0-based in the pool).
+ */
+size_t ce_select_batched_workspace_bytes(int64_t total_items, int32_t U, int32_t q);
+int ce_select_batched(const void *p, ce_dtype dt, int64_t total_items, int32_t M, int32_t C,
+                      int64_t sN, int64_t sM, int64_t sC, const int64_t *offsets, int32_t U,
+                      int32_t q, void *ws, size_t ws_bytes, double *val_out, int64_t *idx_out,
+                      ce_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CE_AMD_CE_H */

@@ -1,0 +1,94 @@
+"""The N>1 path on CPU: world_size-2 gloo process groups run the real sharding,
+packing and all-gather code of ce_amd.dist; the per-rank selection and the
+merge are the oracle's (no GPU here).  The sharded answer must equal the
+single-process global top-q."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ce_oracle as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_local(P, q, base):
+    v, i = O.oracle_select_mc(P.numpy(), q, layout="NMC")
+    vals = np.full(q, np.nan)
+    idx = np.full(q, -1, np.int64)
+    vals[:len(v)] = v
+    idx[:len(i)] = i + base
+    return torch.from_numpy(vals), torch.from_numpy(idx)
+
+
+def _oracle_merge(vals, idx, q):
+    v, i = O.oracle_topq_merge(vals.numpy(), idx.numpy(), q)
+    return torch.from_numpy(v), torch.from_numpy(i)
+
+
+def _worker(rank, world, port, N, q, seed, out):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "consensus-entropy_amd"))
+    from ce_amd import dist as cdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(seed)
+    e = -np.log(rng.random((N, 8, 4)))
+    P = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+    P[::50] = np.floor(P[::50] * 4) / 4  # ties across shard boundaries
+    lo, hi = cdist.shard_range(N, rank, world)
+    v, i = cdist.sharded_select_mc(torch.from_numpy(P[lo:hi]), q, global_offset=lo,
+                                   local_select=_oracle_local, merge=_oracle_merge)
+    out[rank] = (v.numpy().tolist(), i.numpy().tolist())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,q", [(2, 5000, 10), (2, 7, 10), (3, 4001, 25)])
+def test_sharded_equals_global(world, N, q):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), N, q, 1987, out), nprocs=world, join=True)
+    rng = np.random.default_rng(1987)
+    e = -np.log(rng.random((N, 8, 4)))
+    P = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+    P[::50] = np.floor(P[::50] * 4) / 4
+    vg, ig = O.oracle_select_mc(P, q, layout="NMC")
+    for r in range(world):
+        v, i = out[r]
+        assert list(i)[:len(ig)] == ig.tolist()
+        assert all(x == -1 for x in list(i)[len(ig):])
+
+
+def test_shard_range_covers():
+    from ce_amd.dist import shard_range
+
+    for n in (0, 1, 7, 100, 100_000_001):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[k][1] == spans[k + 1][0] for k in range(w - 1))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_pack_roundtrip():
+    from ce_amd.dist import pack, unpack
+
+    v = torch.tensor([np.nan, 1.5, -0.0, 0.25], dtype=torch.float64)
+    i = torch.tensor([3, 1, -1, 9], dtype=torch.int64)
+    buf = torch.cat([pack(v, i), pack(v * 2, i + 100)])
+    vv, ii = unpack(buf, 4, 2)
+    assert torch.equal(ii, torch.cat([i, i + 100]))
+    assert torch.allclose(vv, torch.cat([v, v * 2]), equal_nan=True)
