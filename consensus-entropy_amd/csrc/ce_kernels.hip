@@ -17,11 +17,13 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <cstdlib>
 
 #include "../../include/ce.h"
 #include "ce_device.hpp"
 #include "ce_topq.hpp"
 #include "ce_wide.hpp"
+#include "ce_stream.hpp"
 
 namespace ce {
 
@@ -513,6 +515,55 @@ static int with_committee(const CommArgs& a, F&& f) {
     return CE_EUNSUPPORTED;
 }
 
+// ---- streaming stage 1 (q <= 64): wave-independent, LDS-DMA for item-major ----
+static bool stream_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_STREAM");  // A/B knob: CE_AMD_STREAM=0 -> block-synchronous k_partial
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+static StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx) {
+    StreamArgs s;
+    s.p = a.p;
+    s.N = a.N;
+    s.M = a.M;
+    s.sN = a.sN;
+    s.sM = a.sM;
+    s.sC = a.sC;
+    s.dM = (double)a.M;
+    s.invM = 1.0 / (double)a.M;
+    s.pow2 = (a.M & (a.M - 1)) == 0;
+    s.base_idx = base_idx;
+    const int64_t W = (int64_t)G * 4;
+    s.per_wave = (cdiv(a.N, W) + 63) / 64 * 64;
+    return s;
+}
+
+// Launches the streaming kernel when it applies; returns false otherwise.
+static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st) {
+    if (!stream_enabled() || q > kStreamMaxQ || a.N == 0) return false;
+    const StreamArgs sa = stream_args(a, G, base_idx);
+    const int eb = elem_bytes(a.dt);
+    const int64_t R = (int64_t)a.M * a.C * eb;
+    const bool dense_nmc = a.sC == 1 && a.sM == a.C && a.sN == (int64_t)a.M * a.C && (uintptr_t)a.p % 16 == 0;
+    if (dense_nmc && (R == 256 || R == 512)) {
+#define CE_S(DT_, C_, S_)                                                                                   \
+    if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
+        hipLaunchKernelGGL((k_stream_nmc<DT_, C_, S_>), dim3(G), dim3(256), 0, st, sa, q, w.key, w.idx); \
+        return true;                                                                                      \
+    }
+        CE_S(kF32, 4, 16) CE_S(kF32, 4, 32) CE_S(kBF16, 4, 16) CE_S(kBF16, 4, 32) CE_S(kF64, 4, 32)
+        CE_S(kF32, 8, 16) CE_S(kF32, 8, 32)
+#undef CE_S
+    }
+    const int rc = with_committee(a, [&](auto src) {
+        hipLaunchKernelGGL((k_stream_direct<decltype(src)>), dim3(G), dim3(256), 0, st, src, sa, q, w.key, w.idx);
+    });
+    return rc == CE_OK;
+}
+
 // ---- wide-class dispatch (C not in the register-path set) -------------------
 static WideArgs wide_args(const CommArgs& a) {
     WideArgs w{a.p, a.N, a.M, a.C, a.sN, a.sM, a.sC, (double)a.M, 1.0 / (double)a.M, (a.M & (a.M - 1)) == 0};
@@ -680,7 +731,7 @@ extern "C" int ce_topq_merge(const double* vals, const int64_t* idx, int32_t nli
 extern "C" size_t ce_select_mc_workspace_bytes(int64_t N, int32_t q) { return ce_topq_workspace_bytes(N, q); }
 
 static int mc_partial(const CommArgs& a, int q, int64_t base_idx, void* ws, size_t ws_bytes, double* val_out,
-                      int64_t* idx_out, bool allow_final, int* G_out, hipStream_t st) {
+                      int64_t* idx_out, bool allow_final, int* G_out, bool* final_out, hipStream_t st) {
     int rc = check_comm(a);
     if (rc) return rc;
     rc = check_q(q);
@@ -688,11 +739,14 @@ static int mc_partial(const CommArgs& a, int q, int64_t base_idx, void* ws, size
     const int G = pool_blocks(a.N);
     if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
     WsLists w = carve(ws, G, q);
+    *G_out = G;
+    *final_out = false;
+    if (launch_stream(a, G, q, base_idx, w, st)) return CE_OK;
     Seg sg{nullptr, a.N, G, base_idx};
     const bool fin = allow_final && G == 1;
     rc = committee_partial(a, sg, G, q, w, val_out, idx_out, fin, st);
     if (rc) return dispatch_err(rc, a);
-    *G_out = G;
+    *final_out = fin;
     return CE_OK;
 }
 
@@ -703,9 +757,10 @@ extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, in
     hipStream_t st = (hipStream_t)stream;
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
     int G = 0;
-    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, st);
+    bool fin = false;
+    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, &fin, st);
     if (rc) return rc;
-    if (G > 1) finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
+    if (!fin) finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
     return check_launch("ce_select_mc");
 }
 
@@ -714,7 +769,8 @@ extern "C" int ce_select_mc_partial(const void* p, ce_dtype dt, int64_t N, int32
                                     size_t ws_bytes, ce_stream_t stream) {
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
     int G = 0;
-    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &G, (hipStream_t)stream);
+    bool fin = false;
+    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &G, &fin, (hipStream_t)stream);
     if (rc) return rc;
     return check_launch("ce_select_mc_partial");
 }

@@ -232,7 +232,8 @@ def test_full_size_property(ce):
     g = torch.Generator(device="cuda").manual_seed(1987)
     P = torch.empty((N, M, C), dtype=torch.float32, device="cuda")
     for s in range(0, N, 10_000_000):
-        e = -torch.log(torch.rand((min(N, s + 10_000_000) - s, M, C), device="cuda", generator=g))
+        u = torch.rand((min(N, s + 10_000_000) - s, M, C), device="cuda", generator=g).clamp_min_(1e-30)
+        e = -torch.log(u)
         P[s:s + e.shape[0]] = e / e.sum(-1, keepdim=True)
     vals, idx = ce.ops.select_mc(P, q, "NMC")
     ent = ce.ops.committee_entropy(P, "NMC")
