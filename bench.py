@@ -50,18 +50,26 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_pool(n, M, C, seed, device, chunk=8_000_000):
-    """Dirichlet(1) rows per (item, member); 1% of member rows scaled by U(0.5, 2)."""
-    g = torch.Generator(device=device).manual_seed(seed)
-    P = torch.empty((n, M, C), dtype=torch.float32, device=device)
-    for s in range(0, n, chunk):
-        m = min(n, s + chunk) - s
-        e = -torch.log(torch.rand((m, M, C), device=device, generator=g).clamp_min_(1e-30))
+POOL_CHUNK = 4_000_000
+
+
+def make_pool(lo, hi, M, C, device, seed=1987):
+    """Items [lo, hi) of the synthetic pool: Dirichlet(1) rows per (item,
+    member), 1% of member rows scaled by U(0.5, 2).  Generated in fixed global
+    chunks seeded by chunk number, so every world size sees the SAME pool and
+    the selected positions must agree across N."""
+    P = torch.empty((hi - lo, M, C), dtype=torch.float32, device=device)
+    for c in range(lo // POOL_CHUNK, (hi + POOL_CHUNK - 1) // POOL_CHUNK):
+        c0, c1 = c * POOL_CHUNK, (c + 1) * POOL_CHUNK
+        g = torch.Generator(device=device).manual_seed(seed * 100_003 + c)
+        e = -torch.log(torch.rand((POOL_CHUNK, M, C), device=device, generator=g).clamp_min_(1e-30))
         e /= e.sum(-1, keepdim=True)
-        scale = torch.where(torch.rand((m, M, 1), device=device, generator=g) < 0.01,
-                            torch.rand((m, M, 1), device=device, generator=g) * 1.5 + 0.5,
+        scale = torch.where(torch.rand((POOL_CHUNK, M, 1), device=device, generator=g) < 0.01,
+                            torch.rand((POOL_CHUNK, M, 1), device=device, generator=g) * 1.5 + 0.5,
                             torch.ones((), device=device))
-        P[s:s + m] = e * scale
+        e *= scale
+        a, b = max(lo, c0), min(hi, c1)
+        P[a - lo:b - lo] = e[a - c0:b - c0]
         del e, scale
     return P
 
@@ -140,7 +148,7 @@ def main():
     lo, hi = cdist.shard_range(N, rank, world)
     n_local = hi - lo
     t0 = time.time()
-    P = make_pool(n_local, M, C, 1987 + rank, device)
+    P = make_pool(lo, hi, M, C, device)
     if args.layout == "MNC":
         P = P.permute(1, 0, 2).contiguous()
     torch.cuda.synchronize()

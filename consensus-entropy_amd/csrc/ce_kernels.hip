@@ -101,16 +101,15 @@ __device__ __forceinline__ void seg_range(const Seg& sg, int64_t& s0, int64_t& l
 // Write a finished top-q: either (key, idx) candidates into the workspace, or
 // the final (val, idx) outputs.  Slots past `cnt` are padding (idx -1).
 template <int CAP, bool FINAL>
-__device__ __forceinline__ void write_list(const TopQSmem<CAP>& s, int cnt, int q, uint64_t* wkey,
-                                           int64_t* widx, double* oval, int64_t* oidx) {
+__device__ __forceinline__ void write_list(const TopQSmem<CAP>& s, int cnt, int q, Cand* wc, double* oval,
+                                           int64_t* oidx) {
     for (int r = threadIdx.x; r < q; r += blockDim.x) {
         const bool ok = r < cnt;
         if constexpr (FINAL) {
             oval[r] = ok ? key_to_val(s.key[r]) : __longlong_as_double(0x7ff8000000000000ll);
             oidx[r] = ok ? s.idx[r] : -1;
         } else {
-            wkey[r] = ok ? s.key[r] : 0ull;
-            widx[r] = ok ? s.idx[r] : -1;
+            wc[r] = Cand{ok ? s.key[r] : 0ull, ok ? s.idx[r] : -1};
         }
     }
 }
@@ -119,8 +118,7 @@ __device__ __forceinline__ void write_list(const TopQSmem<CAP>& s, int cnt, int 
 // Stage 1: score + per-block top-q.  One item per thread per round.
 // ---------------------------------------------------------------------------
 template <class Src, int CAP, bool FINAL>
-__global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, uint64_t* __restrict__ wkey,
-                                                 int64_t* __restrict__ widx, double* __restrict__ oval,
+__global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, Cand* __restrict__ wc, double* __restrict__ oval,
                                                  int64_t* __restrict__ oidx) {
     __shared__ TopQSmem<CAP> sm;
     TopQ<CAP, kBS> tq(sm);
@@ -138,16 +136,15 @@ __global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, uint64_
     }
     const int cnt = tq.finish(q);
     const int64_t slot = (int64_t)blockIdx.x * q;
-    write_list<CAP, FINAL>(sm, cnt, q, wkey + slot, widx + slot, oval + (FINAL ? slot : 0),
-                           oidx + (FINAL ? slot : 0));
+    write_list<CAP, FINAL>(sm, cnt, q, wc + slot, oval + (FINAL ? slot : 0), oidx + (FINAL ? slot : 0));
 }
 
 // Wide-class variant: a wave scores 64 consecutive items (one per lane slot),
 // so a block round is still 256 candidates.
 template <int DT, int KMAX, int CAP, bool FINAL>
 __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q,
-                                                      uint64_t* __restrict__ wkey, int64_t* __restrict__ widx,
-                                                      double* __restrict__ oval, int64_t* __restrict__ oidx) {
+                                                      Cand* __restrict__ wc, double* __restrict__ oval,
+                                                      int64_t* __restrict__ oidx) {
     __shared__ TopQSmem<CAP> sm;
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     TopQ<CAP, kBS> tq(sm);
@@ -174,8 +171,7 @@ __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg
     }
     const int cnt = tq.finish(q);
     const int64_t slot = (int64_t)blockIdx.x * q;
-    write_list<CAP, FINAL>(sm, cnt, q, wkey + slot, widx + slot, oval + (FINAL ? slot : 0),
-                           oidx + (FINAL ? slot : 0));
+    write_list<CAP, FINAL>(sm, cnt, q, wc + slot, oval + (FINAL ? slot : 0), oidx + (FINAL ? slot : 0));
 }
 
 // ---------------------------------------------------------------------------
@@ -187,15 +183,18 @@ __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg
 // ---------------------------------------------------------------------------
 template <bool FROM_VALS>
 struct ListSrc {
-    const uint64_t* key;
+    const Cand* c;
     const double* val;
     const int64_t* idx;
     __device__ __forceinline__ void get(int64_t j, uint64_t& k, int64_t& i) const {
-        i = idx[j];
-        if constexpr (FROM_VALS)
+        if constexpr (FROM_VALS) {
+            i = idx[j];
             k = order_key(val[j]);
-        else
-            k = key[j];
+        } else {
+            const Cand x = c[j];
+            k = x.key;
+            i = x.idx;
+        }
     }
 };
 
@@ -218,29 +217,19 @@ __global__ __launch_bounds__(BS) void k_finish(ListSrc<FROM_VALS> src, int nl, i
     __shared__ uint64_t wk[BS / 64];
     __shared__ int64_t wi[BS / 64];
     const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
-    // 1. T = best over full lists of the list's worst entry.
+    const int64_t L = (int64_t)nl * q;
+    // 1. T = best over FULL lists of the list's worst entry; lists are
+    //    best-first, so a list is full iff slot q-1 is used and that slot is
+    //    its worst entry: one load per list.
     uint64_t tk = 0;
-    int64_t ti = INT64_MAX;  // "nothing": worse than any real candidate
+    int64_t ti = INT64_MAX;  // "nothing": admits every candidate
     for (int g = threadIdx.x; g < nl; g += BS) {
-        uint64_t wkk = ~0ull;
-        int64_t wii = -1;
-        bool full = true;
-        for (int r = 0; r < q; ++r) {
-            uint64_t k;
-            int64_t i;
-            src.get(seg0 + (int64_t)g * q + r, k, i);
-            if (i < 0) {
-                full = false;
-                break;
-            }
-            if (better(wkk, wii, k, i)) {
-                wkk = k;
-                wii = i;
-            }
-        }
-        if (full && better(wkk, wii, tk, ti)) {
-            tk = wkk;
-            ti = wii;
+        uint64_t k;
+        int64_t i;
+        src.get(seg0 + (int64_t)g * q + q - 1, k, i);
+        if (i >= 0 && better(k, i, tk, ti)) {
+            tk = k;
+            ti = i;
         }
     }
     wave_best(tk, ti);
@@ -259,27 +248,27 @@ __global__ __launch_bounds__(BS) void k_finish(ListSrc<FROM_VALS> src, int nl, i
     // admit candidates >= T: strictly better than (T.key, T.idx + 1)
     TopQ<CAP, BS> tq(sm);
     tq.init(tk, ti == INT64_MAX ? INT64_MAX : ti + 1);
-    // 2. filter all candidates, IPT per thread in flight
-    const int64_t L = (int64_t)nl * q;
+    // 2. filter every candidate; IPT independent loads per thread in flight
+    //    (addresses clamped, never a branch around a load)
     for (int64_t b0 = 0; b0 < L; b0 += (int64_t)BS * IPT) {
         uint64_t k[IPT];
         int64_t id[IPT];
 #pragma unroll
         for (int u = 0; u < IPT; ++u) {
-            const int64_t j = b0 + (int64_t)u * BS + threadIdx.x;
-            k[u] = 0;
-            id[u] = -1;
-            if (j < L) src.get(seg0 + j, k[u], id[u]);
+            int64_t j = b0 + (int64_t)u * BS + threadIdx.x;
+            const bool in = j < L;
+            src.get(seg0 + (in ? j : L - 1), k[u], id[u]);
+            if (!in) id[u] = -1;
         }
 #pragma unroll
         for (int u = 0; u < IPT; ++u) {
+            if (b0 + (int64_t)u * BS >= L) break;  // block-uniform
             tq.offer(k[u], id[u], id[u] >= 0);
             tq.end_round(q, BS);
         }
     }
     const int cnt = tq.finish(q);
-    write_list<CAP, true>(sm, cnt, q, nullptr, nullptr, oval + (int64_t)blockIdx.x * q,
-                          oidx + (int64_t)blockIdx.x * q);
+    write_list<CAP, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
 }
 
 // ---------------------------------------------------------------------------
@@ -401,14 +390,12 @@ static int pool_blocks(int64_t n) {
 static size_t lists_bytes(int64_t nlists, int q) { return (size_t)nlists * (size_t)q * 16u + 256u; }
 
 struct WsLists {
-    uint64_t* key;
-    int64_t* idx;
+    Cand* c;
 };
 static WsLists carve(void* ws, int64_t nlists, int q) {
     uintptr_t p = ((uintptr_t)ws + 255) & ~(uintptr_t)255;
     WsLists w;
-    w.key = reinterpret_cast<uint64_t*>(p);
-    w.idx = reinterpret_cast<int64_t*>(p + (size_t)nlists * q * 8u);
+    w.c = reinterpret_cast<Cand*>(p);
     return w;
 }
 
@@ -422,18 +409,14 @@ static void launch_partial(const Src& src, const Seg& sg, int grid, int q, WsLis
                            int64_t* oidx, bool final_out, hipStream_t st) {
     if (q <= 256) {
         if (final_out)
-            hipLaunchKernelGGL((k_partial<Src, 1024, true>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
-                               w.idx, oval, oidx);
+            hipLaunchKernelGGL((k_partial<Src, 1024, true>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.c, oval, oidx);
         else
-            hipLaunchKernelGGL((k_partial<Src, 1024, false>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
-                               w.idx, oval, oidx);
+            hipLaunchKernelGGL((k_partial<Src, 1024, false>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.c, oval, oidx);
     } else {
         if (final_out)
-            hipLaunchKernelGGL((k_partial<Src, 4096, true>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
-                               w.idx, oval, oidx);
+            hipLaunchKernelGGL((k_partial<Src, 4096, true>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.c, oval, oidx);
         else
-            hipLaunchKernelGGL((k_partial<Src, 4096, false>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.key,
-                               w.idx, oval, oidx);
+            hipLaunchKernelGGL((k_partial<Src, 4096, false>), dim3(grid), dim3(kBS), 0, st, src, sg, q, w.c, oval, oidx);
     }
 }
 
@@ -442,11 +425,14 @@ static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, d
                           hipStream_t st) {
     const int64_t L = (int64_t)nl * q;
     if (L <= 256 && q <= 128)
-        hipLaunchKernelGGL((k_finish<FROM_VALS, 512, 256, 1>), dim3(segments), dim3(256), 0, st, src, nl, q,
-                           oval, oidx);
+        hipLaunchKernelGGL((k_finish<FROM_VALS, 512, 256, 1>), dim3(segments), dim3(256), 0, st, src, nl, q, oval,
+                           oidx);
+    else if (L <= 4096 && q <= 512)
+        hipLaunchKernelGGL((k_finish<FROM_VALS, 2048, 256, 16>), dim3(segments), dim3(256), 0, st, src, nl, q, oval,
+                           oidx);
     else
-        hipLaunchKernelGGL((k_finish<FROM_VALS, 4096, kFinBS, 8>), dim3(segments), dim3(kFinBS), 0, st, src,
-                           nl, q, oval, oidx);
+        hipLaunchKernelGGL((k_finish<FROM_VALS, 4096, kFinBS, 16>), dim3(segments), dim3(kFinBS), 0, st, src, nl,
+                           q, oval, oidx);
 }
 
 // ---- committee dispatch ----------------------------------------------------
@@ -551,7 +537,7 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
     if (dense_nmc && (R == 256 || R == 512)) {
 #define CE_S(DT_, C_, S_)                                                                                   \
     if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
-        hipLaunchKernelGGL((k_stream_nmc<DT_, C_, S_>), dim3(G), dim3(256), 0, st, sa, q, w.key, w.idx); \
+        hipLaunchKernelGGL((k_stream_nmc<DT_, C_, S_>), dim3(G), dim3(256), 0, st, sa, q, w.c); \
         return true;                                                                                      \
     }
         CE_S(kF32, 4, 16) CE_S(kF32, 4, 32) CE_S(kBF16, 4, 16) CE_S(kBF16, 4, 32) CE_S(kF64, 4, 32)
@@ -559,7 +545,7 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
 #undef CE_S
     }
     const int rc = with_committee(a, [&](auto src) {
-        hipLaunchKernelGGL((k_stream_direct<decltype(src)>), dim3(G), dim3(256), 0, st, src, sa, q, w.key, w.idx);
+        hipLaunchKernelGGL((k_stream_direct<decltype(src)>), dim3(G), dim3(256), 0, st, src, sa, q, w.c);
     });
     return rc == CE_OK;
 }
@@ -601,17 +587,17 @@ static void launch_partial_wide(const CommArgs& a, const Seg& sg, int grid, int 
         if (q <= 256) {
             if (fin)
                 hipLaunchKernelGGL((k_partial_wide<DT, KM, 1024, true>), dim3(grid), dim3(kBS), lds, st, wa, pl, sg,
-                                   q, w.key, w.idx, oval, oidx);
+                                   q, w.c, oval, oidx);
             else
                 hipLaunchKernelGGL((k_partial_wide<DT, KM, 1024, false>), dim3(grid), dim3(kBS), lds, st, wa, pl,
-                                   sg, q, w.key, w.idx, oval, oidx);
+                                   sg, q, w.c, oval, oidx);
         } else {
             if (fin)
                 hipLaunchKernelGGL((k_partial_wide<DT, KM, 4096, true>), dim3(grid), dim3(kBS), lds, st, wa, pl, sg,
-                                   q, w.key, w.idx, oval, oidx);
+                                   q, w.c, oval, oidx);
             else
                 hipLaunchKernelGGL((k_partial_wide<DT, KM, 4096, false>), dim3(grid), dim3(kBS), lds, st, wa, pl,
-                                   sg, q, w.key, w.idx, oval, oidx);
+                                   sg, q, w.c, oval, oidx);
         }
     });
 }
@@ -697,7 +683,7 @@ extern "C" size_t ce_topq_workspace_bytes(int64_t N, int32_t q) {
 
 static int finish_lists(WsLists w, int segments, int nl, int q, double* val_out, int64_t* idx_out,
                         hipStream_t st) {
-    ListSrc<false> ls{w.key, nullptr, w.idx};
+    ListSrc<false> ls{w.c, nullptr, nullptr};
     launch_finish(ls, segments, nl, q, val_out, idx_out, st);
     return CE_OK;
 }
@@ -808,7 +794,7 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     Seg s1{nullptr, N, G1, 0};
     rc = committee_partial(a, s1, G1, q, w, nullptr, nullptr, false, st);
     if (rc) return dispatch_err(rc, a);
-    WsLists w2{w.key + (size_t)G1 * q, w.idx + (size_t)G1 * q};
+    WsLists w2{w.c + (size_t)G1 * q};
     Seg s2{nullptr, N_h, G2, N};
     switch (C) {
 #define CE_T(CC) case CC: launch_partial(TableSrc<CC>{hc, ld_hc}, s2, G2, q, w2, nullptr, nullptr, false, st); break;

@@ -193,7 +193,7 @@ struct StreamArgs {
 // cnt[]) into the block's top-q and write it to the workspace.  Wave 0 does it
 // in LDS scratch that held the wave buffers.
 __device__ inline void block_merge_write(uint64_t (*key)[kStreamCapW], int64_t (*idx)[kStreamCapW], int* cnt,
-                                         int q, uint64_t* wkey, int64_t* widx) {
+                                         int q, Cand* wc) {
     __syncthreads();
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
@@ -218,16 +218,14 @@ __device__ inline void block_merge_write(uint64_t (*key)[kStreamCapW], int64_t (
         __builtin_amdgcn_wave_barrier();
         for (int r = lane; r < q; r += 64) {
             const bool ok = r < n;
-            wkey[r] = ok ? mk[r] : 0ull;
-            widx[r] = ok ? mi[r] : -1;
+            wc[r] = Cand{ok ? mk[r] : 0ull, ok ? mi[r] : -1};
         }
     }
 }
 
 // Item-major, dense rows of 16*S bytes, LDS-DMA staged.
 template <int DT, int C, int S>
-__global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, uint64_t* __restrict__ wkey,
-                                                     int64_t* __restrict__ widx) {
+__global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* __restrict__ wc) {
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
     __shared__ int cnt[4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -258,14 +256,13 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, uint64_
     tq.flush(q);
     if (lane == 0) cnt[w] = tq.count;
     const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, wkey + slot, widx + slot);
+    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot);
 }
 
 // Any strides (vector loads when aligned): member-major [M, N, C] streams
 // coalesced across lanes.
 template <class Src>
-__global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, int q, uint64_t* __restrict__ wkey,
-                                                        int64_t* __restrict__ widx) {
+__global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, int q, Cand* __restrict__ wc) {
     __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
     __shared__ int cnt[4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -286,7 +283,7 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     tq.flush(q);
     if (lane == 0) cnt[w] = tq.count;
     const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, wkey + slot, widx + slot);
+    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot);
 }
 
 }  // namespace ce

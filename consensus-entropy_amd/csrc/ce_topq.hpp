@@ -17,6 +17,12 @@
 
 namespace ce {
 
+// One workspace candidate: order key + position, one 16-B load/store.
+struct __attribute__((aligned(16))) Cand {
+    uint64_t key;
+    int64_t idx;
+};
+
 template <int CAP>
 struct TopQSmem {
     uint64_t key[CAP];

@@ -202,8 +202,14 @@ def test_merge(ce):
     q, nl = 10, 8
     vals = rng.random((nl, q))
     vals[2, 3] = np.nan
-    vals = -np.sort(-vals, axis=1)
+    vals[4, :] = 0.5  # ties across lists
     idx = rng.permutation(10_000)[: nl * q].reshape(nl, q).astype(np.int64)
+    for r in range(nl):  # every list best-first, as the ce_* outputs are (the merge's precondition)
+        o = O.canonical_order(vals[r], q)
+        vals[r], idx[r] = vals[r][o], idx[r][o]
+        ent = np.where(np.isnan(vals[r]), np.inf, vals[r])
+        o2 = np.lexsort((idx[r], -ent))
+        vals[r], idx[r] = vals[r][o2], idx[r][o2]
     idx[5, 7:] = -1
     v, i = ce.ops.topq_merge(dev(vals.ravel()), dev(idx.ravel()), q)
     vo, io = O.oracle_topq_merge(vals.ravel(), idx.ravel(), q)
