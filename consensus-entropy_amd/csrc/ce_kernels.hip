@@ -271,6 +271,102 @@ __global__ __launch_bounds__(BS) void k_finish(ListSrc<FROM_VALS> src, int nl, i
     write_list<CAP, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
 }
 
+// Stage 2 for q <= kHeadsMaxQ (the common case, q = 10).  The lists are
+// best-first, so list heads are each list's best entry; T1 = the q-th best
+// head is an exact lower bound (q distinct lists hold an entry >= T1) and a
+// tight one: the global top-q sit in ~q different lists, so only ~q
+// candidates survive the filter.  Cost: one 1024-entry bitonic sort of the
+// heads + one pass over the (prefetched) candidates + a tiny final sort.
+constexpr int kHeadsBS = 1024;
+constexpr int kHeadsMaxQ = 512;
+
+template <bool FROM_VALS, int IPT>
+__global__ __launch_bounds__(kHeadsBS) void k_finish_heads(ListSrc<FROM_VALS> src, int nl, int q,
+                                                           double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    __shared__ TopQSmem<2048> sm;
+    const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
+    const int64_t L = (int64_t)nl * q;
+    const int tid = threadIdx.x;
+    // prefetch this thread's first IPT candidates (clamped, unconditional)
+    uint64_t k[IPT];
+    int64_t id[IPT];
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) {
+        const int64_t j = (int64_t)u * kHeadsBS + tid;
+        src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);
+        if (j >= L) id[u] = -1;
+    }
+    // best head among this thread's lists (distinct threads -> distinct lists)
+    uint64_t hk = 0;
+    int64_t hi = INT64_MAX;
+    for (int g = tid; g < nl; g += kHeadsBS) {
+        uint64_t kk;
+        int64_t ii;
+        src.get(seg0 + (int64_t)g * q, kk, ii);
+        if (ii >= 0 && better(kk, ii, hk, hi)) {
+            hk = kk;
+            hi = ii;
+        }
+    }
+    TopQ<2048, kHeadsBS> tq(sm);
+    uint64_t tk = 0;
+    int64_t ti = INT64_MAX;
+    if (q <= kHeadsBS / 64) {
+        // q <= 16: each wave's best head (shuffle reduction) comes from a list
+        // of its own; the q-th best of those 16 is the bound.
+        wave_best(hk, hi);
+        const int w = tid >> 6;
+        if ((tid & 63) == 0) {
+            sm.key[w] = hk;
+            sm.idx[w] = hi;
+        }
+        __syncthreads();
+        if (tid < kHeadsBS / 64) {
+            int rank = 0;
+            for (int v = 0; v < kHeadsBS / 64; ++v) rank += better(sm.key[v], sm.idx[v], sm.key[tid], sm.idx[tid]);
+            if (rank == q - 1) {
+                sm.red[0] = sm.key[tid];
+                sm.red[1] = (uint64_t)sm.idx[tid];
+            }
+        }
+        __syncthreads();
+        const int64_t t1 = (int64_t)sm.red[1];
+        if (t1 != INT64_MAX) {  // >= q non-empty lists
+            tk = sm.red[0];
+            ti = t1 + 1;  // admit candidates >= T1
+        }
+    } else {
+        sm.key[tid] = hk;
+        sm.idx[tid] = hi;
+        tq.sort_buffer(kHeadsBS);  // barrier inside, before the first compare
+        __syncthreads();
+        if (q <= kHeadsBS && sm.idx[q - 1] != INT64_MAX) {
+            tk = sm.key[q - 1];
+            ti = sm.idx[q - 1] + 1;
+        }
+    }
+    __syncthreads();
+    tq.init(tk, ti);
+    for (int64_t b0 = 0; b0 < L; b0 += (int64_t)kHeadsBS * IPT) {
+        if (b0 > 0) {
+#pragma unroll
+            for (int u = 0; u < IPT; ++u) {
+                const int64_t j = b0 + (int64_t)u * kHeadsBS + tid;
+                src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);
+                if (j >= L) id[u] = -1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < IPT; ++u) {
+            if (b0 + (int64_t)u * kHeadsBS >= L) break;  // block-uniform
+            tq.offer(k[u], id[u], id[u] >= 0);
+            tq.end_round(q, kHeadsBS);
+        }
+    }
+    const int cnt = tq.finish(q);
+    write_list<2048, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
+}
+
 // ---------------------------------------------------------------------------
 // Per-item entropy to HBM.
 // ---------------------------------------------------------------------------
@@ -424,6 +520,11 @@ template <bool FROM_VALS>
 static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, double* oval, int64_t* oidx,
                           hipStream_t st) {
     const int64_t L = (int64_t)nl * q;
+    if (q <= kHeadsMaxQ && L > 256) {
+        hipLaunchKernelGGL((k_finish_heads<FROM_VALS, 10>), dim3(segments), dim3(kHeadsBS), 0, st, src, nl, q, oval,
+                           oidx);
+        return;
+    }
     if (L <= 256 && q <= 128)
         hipLaunchKernelGGL((k_finish<FROM_VALS, 512, 256, 1>), dim3(segments), dim3(256), 0, st, src, nl, q, oval,
                            oidx);
