@@ -29,7 +29,8 @@ namespace ce {
 
 constexpr int kBS = 256;          // stage-1 block: 4 waves
 constexpr int kFinBS = 1024;      // stage-2 block: 16 waves
-constexpr int kMinRounds = 4;     // >= 4 rounds of kBS items per stage-1 block
+constexpr int kMinRounds = 4;     // >= 4 rounds of kBS items per stage-1 block (batched split)
+constexpr int kMinItemsPerBlock = 64;
 constexpr int kMaxBlocks = 1024;  // stage-1 blocks per pool (4 per CU on 256 CUs)
 
 // ---------------------------------------------------------------------------
@@ -139,12 +140,31 @@ __global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, Cand* _
     write_list<CAP, FINAL>(sm, cnt, q, wc + slot, oval + (FINAL ? slot : 0), oidx + (FINAL ? slot : 0));
 }
 
-// Wide-class variant: a wave scores 64 consecutive items (one per lane slot),
-// so a block round is still 256 candidates.
-template <int DT, int KMAX, int CAP, bool FINAL>
-__global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q,
-                                                      Cand* __restrict__ wc, double* __restrict__ oval,
-                                                      int64_t* __restrict__ oidx) {
+// Wide-class variant of k_partial (q > 64 / segments): a wave scores 64
+// consecutive items (one per lane slot), so a block round is still 256.
+template <int DT, int NPL, bool VEC, int CAP, bool FINAL>
+__global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q, Cand* __restrict__ wc,
+                                                      double* __restrict__ oval, int64_t* __restrict__ oidx);
+
+// Wide classes on the streaming engine (q <= 64): one wave per item, every
+// wave independent, per-wave top-q.  NPL = classes owned per lane (C <= 64*NPL).
+template <int DT, int NPL, bool VEC>
+__device__ __forceinline__ double wide_item(const WideArgs& a, const PwPlan& pl, int64_t it, double* row,
+                                            double* scratch) {
+    if constexpr (VEC) {
+        constexpr int KCH = NPL / ChunkT<DT>::CPC;
+        constexpr int UNR = KCH >= 8 ? 1 : 8 / KCH;
+        return wave_item_entropy_vec<DT, KCH, UNR>(a.p, it * a.sN, a.M, a.C, a.sM, a.dM, a.invM, a.pow2, pl, row,
+                                                   scratch);
+    } else {
+        return wave_item_entropy<DT, NPL>(a.p, it * a.sN, a.M, a.C, a.sM, a.sC, a.dM, a.invM, a.pow2, pl, row,
+                                          scratch, nullptr);
+    }
+}
+
+template <int DT, int NPL, bool VEC, int CAP, bool FINAL>
+__global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q, Cand* __restrict__ wc,
+                                                      double* __restrict__ oval, int64_t* __restrict__ oidx) {
     __shared__ TopQSmem<CAP> sm;
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     TopQ<CAP, kBS> tq(sm);
@@ -161,8 +181,7 @@ __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg
         for (int j = 0; j < 64; ++j) {
             const int64_t it = wbase + j;
             if (it >= hi) break;  // wave-uniform
-            const double h = wave_item_entropy<DT, KMAX>(a.p, it * a.sN, a.M, a.C, a.sM, a.sC, a.dM, a.invM,
-                                                         a.pow2, pl, row, scratch, nullptr);
+            const double h = wide_item<DT, NPL, VEC>(a, pl, it, row, scratch);
             if (lane == j) mykey = order_key(h);
         }
         const int64_t i = i0 + threadIdx.x;
@@ -172,6 +191,51 @@ __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg
     const int cnt = tq.finish(q);
     const int64_t slot = (int64_t)blockIdx.x * q;
     write_list<CAP, FINAL>(sm, cnt, q, wc + slot, oval + (FINAL ? slot : 0), oidx + (FINAL ? slot : 0));
+}
+
+template <int DT, int NPL, bool VEC>
+__global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, StreamArgs sa, int q,
+                                                     Cand* __restrict__ wc) {
+    __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
+    __shared__ int cnt[4];
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+    int64_t lo = gw * sa.per_wave;
+    int64_t hi = lo + sa.per_wave;
+    if (hi > a.N) hi = a.N;
+    if (lo > hi) lo = hi;
+    WaveTopQ<kStreamCapW> tq;
+    tq.init(sm.key[w], sm.idx[w]);
+    for (int64_t t0 = lo; t0 < hi; t0 += 64) {
+        uint64_t mykey = 0;
+        for (int j = 0; j < 64; ++j) {
+            const int64_t it = t0 + j;
+            if (it >= hi) break;  // wave-uniform
+            const double h = wide_item<DT, NPL, VEC>(a, pl, it, row, scratch);
+            if (lane == j) mykey = order_key(h);
+        }
+        const int64_t i = t0 + lane;
+        tq.offer(mykey, i + sa.base_idx, i < hi, q);
+    }
+    tq.flush(q);
+    if (lane == 0) cnt[w] = tq.count;
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot, sa.nlists);
+}
+
+template <int DT, int NPL, bool VEC>
+__global__ __launch_bounds__(kBS) void k_wide_entropy_v(WideArgs a, PwPlan pl, double* __restrict__ ent) {
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    const int w = threadIdx.x >> 6;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < a.N; i += (int64_t)gridDim.x * 4) {
+        const double h = wide_item<DT, NPL, VEC>(a, pl, i, row, scratch);
+        if ((threadIdx.x & 63) == 0) ent[i] = h;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -477,7 +541,9 @@ static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // stage-1 blocks for a pool of n items (host arithmetic only: ws sizing and
 // launches agree by construction)
 static int pool_blocks(int64_t n) {
-    int64_t g = cdiv(n, (int64_t)kBS * kMinRounds);
+    // one 64-item tile per wave at least; up to 1024 blocks (4 per CU), so wide
+    // items (tens of KB each) still fill the chip
+    int64_t g = cdiv(n, (int64_t)kMinItemsPerBlock);
     if (g < 1) g = 1;
     if (g > kMaxBlocks) g = kMaxBlocks;
     return (int)g;
@@ -602,6 +668,66 @@ static int with_committee(const CommArgs& a, F&& f) {
     return CE_EUNSUPPORTED;
 }
 
+// ---- wide-class dispatch (C not in the register-path set) -------------------
+static WideArgs wide_args(const CommArgs& a) {
+    WideArgs w{a.p, a.N, a.M, a.C, a.sN, a.sM, a.sC, (double)a.M, 1.0 / (double)a.M, (a.M & (a.M - 1)) == 0};
+    return w;
+}
+static size_t wide_lds_bytes(int C) { return (size_t)4 * wide_lds_doubles(C) * sizeof(double); }
+
+static bool wide_vec_ok(const CommArgs& a) {
+    const int eb = elem_bytes(a.dt);
+    return a.sC == 1 && (a.C * eb) % 16 == 0 && (a.sM * eb) % 16 == 0 && (a.sN * eb) % 16 == 0 &&
+           (uintptr_t)a.p % 16 == 0;
+}
+
+// f(dt, npl, vec) with compile-time values
+template <class F>
+static int with_wide_v(const CommArgs& a, F&& f) {
+    if (a.C > kWideMaxC) return CE_EUNSUPPORTED;
+    const bool vec = wide_vec_ok(a);
+#define CE_WV(DT_, NPL_)                                                                              \
+    if (vec) f(std::integral_constant<int, DT_>(), std::integral_constant<int, NPL_>(), std::true_type()); \
+    else f(std::integral_constant<int, DT_>(), std::integral_constant<int, NPL_>(), std::false_type());
+#define CE_WD(DT_)                                   \
+    if (a.dt == DT_) {                               \
+        if (a.C <= 512) { CE_WV(DT_, 8) }            \
+        else if (a.C <= 1024) { CE_WV(DT_, 16) }     \
+        else { CE_WV(DT_, 32) }                      \
+        return CE_OK;                                \
+    }
+    CE_WD(kF32) CE_WD(kF64) CE_WD(kBF16)
+#undef CE_WD
+#undef CE_WV
+    return CE_EUNSUPPORTED;
+}
+
+static void launch_partial_wide(const CommArgs& a, const Seg& sg, int grid, int q, WsLists w, double* oval,
+                                int64_t* oidx, bool fin, hipStream_t st) {
+    const WideArgs wa = wide_args(a);
+    const PwPlan pl = pw_plan(a.C);
+    const size_t lds = wide_lds_bytes(a.C);
+    with_wide_v(a, [&](auto dt, auto npl, auto vec) {
+        constexpr int DT = decltype(dt)::value, NPL = decltype(npl)::value;
+        constexpr bool VEC = decltype(vec)::value;
+        if (q <= 256) {
+            if (fin)
+                hipLaunchKernelGGL((k_partial_wide<DT, NPL, VEC, 1024, true>), dim3(grid), dim3(kBS), lds, st, wa, pl,
+                                   sg, q, w.c, oval, oidx);
+            else
+                hipLaunchKernelGGL((k_partial_wide<DT, NPL, VEC, 1024, false>), dim3(grid), dim3(kBS), lds, st, wa,
+                                   pl, sg, q, w.c, oval, oidx);
+        } else {
+            if (fin)
+                hipLaunchKernelGGL((k_partial_wide<DT, NPL, VEC, 4096, true>), dim3(grid), dim3(kBS), lds, st, wa, pl,
+                                   sg, q, w.c, oval, oidx);
+            else
+                hipLaunchKernelGGL((k_partial_wide<DT, NPL, VEC, 4096, false>), dim3(grid), dim3(kBS), lds, st, wa,
+                                   pl, sg, q, w.c, oval, oidx);
+        }
+    });
+}
+
 // ---- streaming stage 1 (q <= 64): wave-independent, LDS-DMA for item-major ----
 static bool stream_enabled() {
     static const bool on = [] {
@@ -609,6 +735,30 @@ static bool stream_enabled() {
         return !(e && e[0] == '0');
     }();
     return on;
+}
+
+// Blocks of `kernel` resident on the whole device (occupancy API x CUs), cached.
+static int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
+template <class K>
+static int resident_grid(K kernel, size_t dyn_lds, int cap) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, dyn_lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    (void)hipGetLastError();
+    const int g = per_cu * device_cus();
+    return g < cap ? g : cap;
 }
 
 static StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx) {
@@ -623,84 +773,52 @@ static StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx) {
     s.invM = 1.0 / (double)a.M;
     s.pow2 = (a.M & (a.M - 1)) == 0;
     s.base_idx = base_idx;
-    const int64_t W = (int64_t)G * 4;
-    s.per_wave = (cdiv(a.N, W) + 63) / 64 * 64;
+    s.nlists = G;
+    s.per_wave = 0;
     return s;
+}
+
+// the grid actually launched (<= G workspace lists) and its per-wave share
+static void stream_grid(StreamArgs& s, int grid) {
+    const int64_t W = (int64_t)grid * 4;
+    s.per_wave = (cdiv(s.N, W) + 63) / 64 * 64;
 }
 
 // Launches the streaming kernel when it applies; returns false otherwise.
 static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st) {
     if (!stream_enabled() || q > kStreamMaxQ || a.N == 0) return false;
-    const StreamArgs sa = stream_args(a, G, base_idx);
+    StreamArgs sa = stream_args(a, G, base_idx);
     const int eb = elem_bytes(a.dt);
     const int64_t R = (int64_t)a.M * a.C * eb;
     const bool dense_nmc = a.sC == 1 && a.sM == a.C && a.sN == (int64_t)a.M * a.C && (uintptr_t)a.p % 16 == 0;
     if (dense_nmc && (R == 256 || R == 512)) {
 #define CE_S(DT_, C_, S_)                                                                                   \
     if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
-        hipLaunchKernelGGL((k_stream_nmc<DT_, C_, S_>), dim3(G), dim3(256), 0, st, sa, q, w.c); \
+        const int grid = resident_grid(k_stream_nmc<DT_, C_, S_>, 0, G);                                 \
+        stream_grid(sa, grid);                                                                            \
+        hipLaunchKernelGGL((k_stream_nmc<DT_, C_, S_>), dim3(grid), dim3(256), 0, st, sa, q, w.c);        \
         return true;                                                                                      \
     }
         CE_S(kF32, 4, 16) CE_S(kF32, 4, 32) CE_S(kBF16, 4, 16) CE_S(kBF16, 4, 32) CE_S(kF64, 4, 32)
         CE_S(kF32, 8, 16) CE_S(kF32, 8, 32)
 #undef CE_S
     }
-    const int rc = with_committee(a, [&](auto src) {
-        hipLaunchKernelGGL((k_stream_direct<decltype(src)>), dim3(G), dim3(256), 0, st, src, sa, q, w.c);
+    int rc = with_committee(a, [&](auto src) {
+        const int grid = resident_grid(k_stream_direct<decltype(src), 2>, 0, G);
+        stream_grid(sa, grid);
+        hipLaunchKernelGGL((k_stream_direct<decltype(src), 2>), dim3(grid), dim3(256), 0, st, src, sa, q, w.c);
     });
-    return rc == CE_OK;
-}
-
-// ---- wide-class dispatch (C not in the register-path set) -------------------
-static WideArgs wide_args(const CommArgs& a) {
-    WideArgs w{a.p, a.N, a.M, a.C, a.sN, a.sM, a.sC, (double)a.M, 1.0 / (double)a.M, (a.M & (a.M - 1)) == 0};
-    return w;
-}
-static size_t wide_lds_bytes(int C) { return (size_t)4 * wide_lds_doubles(C) * sizeof(double); }
-
-// f(dt_tag, kmax_tag) with compile-time DT / KMAX
-template <class F>
-static int with_wide(const CommArgs& a, F&& f) {
-    if (a.C > kWideMaxC) return CE_EUNSUPPORTED;
-    const int k = (a.C + 63) / 64;
-#define CE_W(DT_)                                                                   \
-    if (a.dt == DT_) {                                                              \
-        if (k <= 1) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 1>());        \
-        else if (k <= 2) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 2>());   \
-        else if (k <= 4) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 4>());   \
-        else if (k <= 8) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 8>());   \
-        else if (k <= 16) f(std::integral_constant<int, DT_>(), std::integral_constant<int, 16>()); \
-        else f(std::integral_constant<int, DT_>(), std::integral_constant<int, 32>());              \
-        return CE_OK;                                                               \
-    }
-    CE_W(kF32) CE_W(kF64) CE_W(kBF16)
-#undef CE_W
-    return CE_EUNSUPPORTED;
-}
-
-static void launch_partial_wide(const CommArgs& a, const Seg& sg, int grid, int q, WsLists w, double* oval,
-                                int64_t* oidx, bool fin, hipStream_t st) {
+    if (rc == CE_OK) return true;
     const WideArgs wa = wide_args(a);
     const PwPlan pl = pw_plan(a.C);
     const size_t lds = wide_lds_bytes(a.C);
-    with_wide(a, [&](auto dt, auto km) {
-        constexpr int DT = decltype(dt)::value, KM = decltype(km)::value;
-        if (q <= 256) {
-            if (fin)
-                hipLaunchKernelGGL((k_partial_wide<DT, KM, 1024, true>), dim3(grid), dim3(kBS), lds, st, wa, pl, sg,
-                                   q, w.c, oval, oidx);
-            else
-                hipLaunchKernelGGL((k_partial_wide<DT, KM, 1024, false>), dim3(grid), dim3(kBS), lds, st, wa, pl,
-                                   sg, q, w.c, oval, oidx);
-        } else {
-            if (fin)
-                hipLaunchKernelGGL((k_partial_wide<DT, KM, 4096, true>), dim3(grid), dim3(kBS), lds, st, wa, pl, sg,
-                                   q, w.c, oval, oidx);
-            else
-                hipLaunchKernelGGL((k_partial_wide<DT, KM, 4096, false>), dim3(grid), dim3(kBS), lds, st, wa, pl,
-                                   sg, q, w.c, oval, oidx);
-        }
+    rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
+        auto kern = k_stream_wide<decltype(dt)::value, decltype(npl)::value, decltype(vec)::value>;
+        const int grid = resident_grid(kern, lds, G);
+        stream_grid(sa, grid);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
     });
+    return rc == CE_OK;
 }
 
 // Committee stage 1 for any supported shape: register path or wide path.
@@ -740,9 +858,10 @@ extern "C" int ce_committee_entropy(const void* p, ce_dtype dt, int64_t N, int32
         const PwPlan pl = pw_plan(C);
         const size_t lds = wide_lds_bytes(C);
         const int wgrid = (int)std::min<int64_t>(cdiv(N, 4), 8192);
-        rc = with_wide(a, [&](auto dt, auto km) {
-            hipLaunchKernelGGL((k_wide_entropy<decltype(dt)::value, decltype(km)::value>), dim3(wgrid), dim3(256),
-                               lds, st, wa, pl, mean_or_null, ent);
+        if (mean_or_null) return fail(CE_EUNSUPPORTED, "mean output for C=%d is not implemented", C);
+        rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
+            hipLaunchKernelGGL((k_wide_entropy_v<decltype(dt)::value, decltype(npl)::value, decltype(vec)::value>),
+                               dim3(wgrid), dim3(256), lds, st, wa, pl, ent);
         });
     }
     if (rc) return dispatch_err(rc, a);
@@ -935,6 +1054,13 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     const int64_t nl = (int64_t)bpu * U;
     if (!ws || ws_bytes < lists_bytes(nl, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
+    if (stream_enabled() && q <= kStreamMaxQ) {
+        rc = with_committee(a, [&](auto src) {
+            hipLaunchKernelGGL((k_stream_seg<decltype(src), 4>), dim3(U), dim3(256), 0, st, src, offsets, q, val_out,
+                               idx_out);
+        });
+        if (rc == CE_OK) return check_launch("ce_select_batched");
+    }
     WsLists w = carve(ws, nl, q);
     Seg sg{offsets, total_items, bpu, 0};
     const bool fin = bpu == 1;

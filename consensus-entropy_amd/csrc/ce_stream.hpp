@@ -187,13 +187,19 @@ struct StreamArgs {
     bool pow2;
     int64_t base_idx;
     int64_t per_wave;  // items per wave (multiple of 64)
+    int nlists;        // workspace lists (>= gridDim.x); lists past the grid are written empty
 };
 
 // Merge the block's 4 wave lists (each best-first, <= q entries, counts in
 // cnt[]) into the block's top-q and write it to the workspace.  Wave 0 does it
 // in LDS scratch that held the wave buffers.
 __device__ inline void block_merge_write(uint64_t (*key)[kStreamCapW], int64_t (*idx)[kStreamCapW], int* cnt,
-                                         int q, Cand* wc) {
+                                         int q, Cand* wc, int nlists, double* oval = nullptr,
+                                         int64_t* oidx = nullptr) {
+    // empty lists for the workspace slots no block of this (occupancy-sized)
+    // grid owns: b + gridDim.x, b + 2*gridDim.x, ...
+    for (int64_t s = (int64_t)blockIdx.x + gridDim.x; s < nlists; s += gridDim.x)
+        for (int r = threadIdx.x; r < q; r += blockDim.x) wc[(s - blockIdx.x) * q + r] = Cand{0ull, -1};
     __syncthreads();
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
@@ -218,7 +224,12 @@ __device__ inline void block_merge_write(uint64_t (*key)[kStreamCapW], int64_t (
         __builtin_amdgcn_wave_barrier();
         for (int r = lane; r < q; r += 64) {
             const bool ok = r < n;
-            wc[r] = Cand{ok ? mk[r] : 0ull, ok ? mi[r] : -1};
+            if (oval) {
+                oval[r] = ok ? key_to_val(mk[r]) : __longlong_as_double(0x7ff8000000000000ll);
+                oidx[r] = ok ? mi[r] : -1;
+            } else {
+                wc[r] = Cand{ok ? mk[r] : 0ull, ok ? mi[r] : -1};
+            }
         }
     }
 }
@@ -256,12 +267,32 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     tq.flush(q);
     if (lane == 0) cnt[w] = tq.count;
     const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot);
+    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot, a.nlists);
 }
 
 // Any strides (vector loads when aligned): member-major [M, N, C] streams
-// coalesced across lanes.
-template <class Src>
+// coalesced across lanes.  IPL items per lane per iteration keep IPL x M
+// member loads in flight per lane.
+template <class Src, int IPL>
+__device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, int64_t hi, int64_t rel, int q,
+                                                    WaveTopQ<kStreamCapW>& tq) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t t0 = lo; t0 < hi; t0 += 64 * IPL) {
+        uint64_t k[IPL];
+#pragma unroll
+        for (int u = 0; u < IPL; ++u) {
+            const int64_t i = t0 + 64 * u + lane;
+            k[u] = src.key(i < hi ? i : hi - 1);  // clamped: every lane loads, no branch per item
+        }
+#pragma unroll
+        for (int u = 0; u < IPL; ++u) {
+            const int64_t i = t0 + 64 * u + lane;
+            tq.offer(k[u], i + rel, i < hi, q);
+        }
+    }
+}
+
+template <class Src, int IPL>
 __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, int q, Cand* __restrict__ wc) {
     __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
     __shared__ int cnt[4];
@@ -273,17 +304,35 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     if (lo > hi) lo = hi;
     WaveTopQ<kStreamCapW> tq;
     tq.init(sm.key[w], sm.idx[w]);
-    for (int64_t t0 = lo; t0 < hi; t0 += 64) {
-        const int64_t i = t0 + lane;
-        const bool valid = i < hi;
-        uint64_t k = 0;
-        if (valid) k = src.key(i);
-        tq.offer(k, i + a.base_idx, valid, q);
-    }
+    stream_direct_range<Src, IPL>(src, lo, hi, a.base_idx, q, tq);
     tq.flush(q);
     if (lane == 0) cnt[w] = tq.count;
     const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot);
+    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot, a.nlists);
+}
+
+// Batched pools (amg_test.py:345's per-user loop in one launch): block u owns
+// segment [offsets[u], offsets[u+1]), its 4 waves split it, and the block's
+// merged top-q is the user's final answer (user-local positions).
+template <class Src, int IPL>
+__global__ __launch_bounds__(256) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int q,
+                                                     double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
+    __shared__ int cnt[4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t s0 = offsets[blockIdx.x], s1 = offsets[blockIdx.x + 1];
+    const int64_t len = s1 > s0 ? s1 - s0 : 0;
+    const int64_t per = ((len + 3) / 4 + 63) / 64 * 64;
+    int64_t lo = s0 + w * per;
+    int64_t hi = lo + per < s1 ? lo + per : s1;
+    if (lo > hi) lo = hi;
+    WaveTopQ<kStreamCapW> tq;
+    tq.init(sm.key[w], sm.idx[w]);
+    stream_direct_range<Src, IPL>(src, lo, hi, -s0, q, tq);
+    tq.flush(q);
+    if (lane == 0) cnt[w] = tq.count;
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    block_merge_write(sm.key, sm.idx, cnt, q, nullptr, 0, oval + slot, oidx + slot);
 }
 
 }  // namespace ce

@@ -169,6 +169,108 @@ __device__ inline double wave_item_entropy(const void* p, int64_t off, int M, in
     return h;
 }
 
+// Vectorised variant: member rows of C*size bytes, 16-B aligned, C*size % 16
+// == 0.  Lane l owns 16-B chunks l, l+64, ... (CPC classes each); UNR member
+// rows are in flight per lane before the in-order adds.
+template <int DT>
+struct ChunkT;
+template <>
+struct ChunkT<kF32> {
+    static constexpr int CPC = 4;
+};
+template <>
+struct ChunkT<kF64> {
+    static constexpr int CPC = 2;
+};
+template <>
+struct ChunkT<kBF16> {
+    static constexpr int CPC = 8;
+};
+
+template <int DT>
+__device__ __forceinline__ void chunk_add(const uint32_t (&u)[4], double* acc) {
+    if constexpr (DT == kF32) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += (double)__uint_as_float(u[e]);
+    } else if constexpr (DT == kF64) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            acc[e] += __longlong_as_double((long long)(((uint64_t)u[2 * e + 1] << 32) | u[2 * e]));
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf16_to_f64((u[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+    }
+}
+
+template <int DT, int KCH, int UNR>
+__device__ inline double wave_item_entropy_vec(const void* p, int64_t off, int M, int C, int64_t sM, double dM,
+                                               double invM, bool pow2, const PwPlan& pl, double* row,
+                                               double* scratch) {
+    constexpr int CPC = ChunkT<DT>::CPC;
+    constexpr int EB = 16 / CPC;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int K = C / CPC;  // chunks per member row
+    const char* base = static_cast<const char*>(p) + off * EB;
+    double acc[KCH * CPC];
+#pragma unroll
+    for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
+    int m = 0;
+    for (; m + UNR <= M; m += UNR) {
+        uint32_t v[UNR][KCH][4];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+#pragma unroll
+            for (int kk = 0; kk < KCH; ++kk) {
+                const int ch = lane + 64 * kk;
+                const int chs = ch < K ? ch : K - 1;
+                const u32x4 x = __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x4*>(base + ((int64_t)(m + u) * sM) * EB) + chs);
+                v[u][kk][0] = x.x;
+                v[u][kk][1] = x.y;
+                v[u][kk][2] = x.z;
+                v[u][kk][3] = x.w;
+            }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+#pragma unroll
+            for (int kk = 0; kk < KCH; ++kk) chunk_add<DT>(v[u][kk], acc + kk * CPC);
+    }
+    for (; m < M; ++m) {
+#pragma unroll
+        for (int kk = 0; kk < KCH; ++kk) {
+            const int ch = lane + 64 * kk;
+            const int chs = ch < K ? ch : K - 1;
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + ((int64_t)m * sM) * EB) + chs);
+            const uint32_t t[4] = {x.x, x.y, x.z, x.w};
+            chunk_add<DT>(t, acc + kk * CPC);
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < KCH; ++kk) {
+        const int ch = lane + 64 * kk;
+#pragma unroll
+        for (int e = 0; e < CPC; ++e) {
+            acc[kk * CPC + e] = div_members(acc[kk * CPC + e], dM, invM, pow2);
+            if (ch < K) row[ch * CPC + e] = acc[kk * CPC + e];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double s = wave_row_sum(row, pl, scratch);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kk = 0; kk < KCH; ++kk) {
+        const int ch = lane + 64 * kk;
+#pragma unroll
+        for (int e = 0; e < CPC; ++e)
+            if (ch < K) row[ch * CPC + e] = entr(1.0 * acc[kk * CPC + e] / s);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double h = wave_row_sum(row, pl, scratch);
+    __builtin_amdgcn_wave_barrier();
+    return h;
+}
+
 struct WideArgs {
     const void* p;
     int64_t N;
@@ -180,19 +282,5 @@ struct WideArgs {
 
 // LDS per wave: C row + scratch.
 __host__ __device__ constexpr int wide_lds_doubles(int C) { return ((C + kPwMaxLeaves + 8 + 1) / 2) * 2; }
-
-template <int DT, int KMAX>
-__global__ __launch_bounds__(256) void k_wide_entropy(WideArgs a, PwPlan pl, double* __restrict__ mean_out,
-                                                      double* __restrict__ ent) {
-    extern __shared__ __attribute__((aligned(16))) double wsm[];
-    const int w = threadIdx.x >> 6;
-    double* row = wsm + w * wide_lds_doubles(a.C);
-    double* scratch = row + a.C;
-    for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < a.N; i += (int64_t)gridDim.x * 4) {
-        const double h = wave_item_entropy<DT, KMAX>(a.p, i * a.sN, a.M, a.C, a.sM, a.sC, a.dM, a.invM, a.pow2,
-                                                     pl, row, scratch, mean_out ? mean_out + i * a.C : nullptr);
-        if ((threadIdx.x & 63) == 0) ent[i] = h;
-    }
-}
 
 }  // namespace ce

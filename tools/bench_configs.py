@@ -1,0 +1,115 @@
+"""Per-config measurements for BASELINE.json configs[0..4] (bench.py's JSON line
+is configs[3]; this prints one JSON line per config for DESIGN.md).
+
+Timing: HIP events on the launch stream around `reps` back-to-back calls of
+the op with inputs resident in HBM; algorithmic bytes per SURVEY.md §8(d).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "consensus-entropy_amd")]
+import torch  # noqa: E402
+
+import ce_amd.ops as ops  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps, graph=True):
+    """Seconds per call.  graph=True: one call captured in a HIP graph and
+    replayed, so Python/ctypes launch overhead is excluded (device time of the
+    call's kernels and the gaps between them)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        run = g.replay
+    else:
+        run = fn
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        run()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e-3
+
+
+def dirichlet(shape, dtype=torch.float32, gen=None):
+    e = -torch.log(torch.rand(shape, device="cuda", generator=gen).clamp_min_(1e-30))
+    return (e / e.sum(-1, keepdim=True)).to(dtype)
+
+
+def report(name, items, bytes_, t, extra=None):
+    d = {"config": name, "items": items, "s_per_call": t, "items_per_s": items / t,
+         "GB_per_s": bytes_ / t / 1e9, "frac_hbm": bytes_ / t / 1e9 / PEAK}
+    d.update(extra or {})
+    print(json.dumps(d), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="0,1,2,4")
+    args = ap.parse_args()
+    only = {int(x) for x in args.only.split(",")}
+    g = torch.Generator(device="cuda").manual_seed(1987)
+    q = 10
+    if 0 in only:  # configs[0]: 4-member committee x 1608 x 4, mixed f32/f64 -> f64 stack
+        P = dirichlet((4, 1608, 4), torch.float64, g)
+        t = timed(lambda: ops.select_mc(P, q, "MNC"), 200)
+        report("configs[0] mc 4x1608x4 f64 (latency)", 1608, P.numel() * 8, t)
+    if 1 in only:  # configs[1]: hc votes 1608 x 665 int8 + mix with a 4x1608x4 committee
+        for dens in (0.03, 1.0):
+            v = torch.randint(0, 4, (1608, 665), device="cuda", generator=g, dtype=torch.int64).to(torch.int8)
+            miss = torch.rand((1608, 665), device="cuda", generator=g) >= dens
+            v[miss] = -1
+            v[:, 0] = 1
+            t = timed(lambda: ops.vote_table(v), 200)
+            report(f"configs[1] hc table 1608x665 int8 density {dens}", 1608, v.numel(), t)
+            freq, _ = ops.vote_table(v)
+            Hn = freq.unsqueeze(1)
+            t = timed(lambda: ops.select_mc(Hn, q, "NMC"), 200)
+            report("configs[1] hc select over the 1608x4 table", 1608, freq.numel() * 8, t)
+            P = dirichlet((4, 1608, 4), torch.float32, g)
+            t = timed(lambda: ops.select_mix(P, freq, q, "MNC"), 200)
+            report("configs[1] mix [4x1608x4 f32 ; 1608x4 hc]", 3216, P.numel() * 4 + freq.numel() * 8, t)
+    if 2 in only:  # configs[2]: 500 users x 4 members x 1608 x 4, q per user, one launch
+        U, Nu = 500, 1608
+        P = dirichlet((4, U * Nu, 4), torch.float32, g)
+        offs = torch.arange(0, U + 1, device="cuda", dtype=torch.int64) * Nu
+        t = timed(lambda: ops.select_batched(P, offs, q, "MNC"), 50)
+        report("configs[2] batched 500 users x 4 x 1608 x 4 f32", U * Nu, P.numel() * 4, t)
+        sizes = torch.randint(128, 1609, (U,), generator=torch.Generator().manual_seed(1987))
+        offs_r = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(sizes, 0)]).cuda()
+        n = int(offs_r[-1])
+        Pr = P[:, :n].contiguous()
+        t = timed(lambda: ops.select_batched(Pr, offs_r, q, "MNC"), 50)
+        report("configs[2] batched ragged 500 users (N_u in [128,1608])", n, Pr.numel() * 4, t)
+    if 4 in only:  # configs[4]: 50M x 32 x 1000 bf16 (3.2 TB): one resident chunk, re-scored per chunk
+        Nc, M, C = 200_000, 32, 1000
+        chunk = torch.empty((Nc, M, C), dtype=torch.bfloat16, device="cuda")
+        for s in range(0, Nc, 20_000):
+            chunk[s:s + 20_000] = dirichlet((20_000, M, C), torch.bfloat16, g)
+        torch.cuda.synchronize()
+        total = 50_000_000
+        nchunks = 5
+        t0 = time.time()
+        t = timed(lambda: ops.select_mc(chunk, q, "NMC"), nchunks)
+        report("configs[4] wide 32x1000 bf16, per 200K-item chunk", Nc, chunk.numel() * 2, t,
+               {"est_full_50M_s": t * total / Nc, "wall": time.time() - t0})
+
+
+if __name__ == "__main__":
+    main()
