@@ -144,6 +144,15 @@ struct MemberLoad<kF32, C, true> {
             acc[4 * k + 3] += (double)v[k].w;
         }
     }
+    __device__ __forceinline__ void add_masked(double (&acc)[C], bool live) const {
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) {
+            acc[4 * k + 0] += live ? (double)v[k].x : 0.0;
+            acc[4 * k + 1] += live ? (double)v[k].y : 0.0;
+            acc[4 * k + 2] += live ? (double)v[k].z : 0.0;
+            acc[4 * k + 3] += live ? (double)v[k].w : 0.0;
+        }
+    }
 };
 
 template <int C>
@@ -160,6 +169,13 @@ struct MemberLoad<kF64, C, true> {
         for (int k = 0; k < C / 2; ++k) {
             acc[2 * k + 0] += v[k].x;
             acc[2 * k + 1] += v[k].y;
+        }
+    }
+    __device__ __forceinline__ void add_masked(double (&acc)[C], bool live) const {
+#pragma unroll
+        for (int k = 0; k < C / 2; ++k) {
+            acc[2 * k + 0] += live ? v[k].x : 0.0;
+            acc[2 * k + 1] += live ? v[k].y : 0.0;
         }
     }
 };
@@ -180,6 +196,15 @@ struct MemberLoad<kBF16, C, true> {
             acc[4 * k + 1] += bf16_to_f64(v[k].x >> 16);
             acc[4 * k + 2] += bf16_to_f64(v[k].y & 0xffffu);
             acc[4 * k + 3] += bf16_to_f64(v[k].y >> 16);
+        }
+    }
+    __device__ __forceinline__ void add_masked(double (&acc)[C], bool live) const {
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) {
+            acc[4 * k + 0] += live ? bf16_to_f64(v[k].x & 0xffffu) : 0.0;
+            acc[4 * k + 1] += live ? bf16_to_f64(v[k].x >> 16) : 0.0;
+            acc[4 * k + 2] += live ? bf16_to_f64(v[k].y & 0xffffu) : 0.0;
+            acc[4 * k + 3] += live ? bf16_to_f64(v[k].y >> 16) : 0.0;
         }
     }
 };
@@ -204,32 +229,57 @@ struct MemberLoad<DT, C, false> {
 #pragma unroll
         for (int c = 0; c < C; ++c) acc[c] += v[c];
     }
+    __device__ __forceinline__ void add_masked(double (&acc)[C], bool live) const {
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] += live ? v[c] : 0.0;
+    }
 };
 
-// Consensus mean of one item over M members, member-sequential (amg_test.py:441),
-// with up to UNR member loads in flight before the in-order adds.
+// Consensus means of IPL items over M members, member-sequential per item
+// (amg_test.py:441).  Members are loaded in batches of UNR for all IPL items
+// before any add, so UNR*IPL loads are in flight per lane.  A batch past M
+// re-loads member M-1 (always in bounds, no branch around a load) and adds
+// +0.0 instead: acc starts at +0.0 and a round-to-nearest sum is -0.0 only if
+// both operands are, so acc is never -0.0 and x + 0.0 == x exactly -- the
+// padding is a bit-exact no-op.
+template <int DT, int C, bool VEC, int UNR, int IPL>
+__device__ __forceinline__ void committee_mean_multi(const void* p, const int64_t (&item_off)[IPL], int M,
+                                                     int64_t sM, int64_t sC, double dM, double invM, bool pow2,
+                                                     double (&mean)[IPL][C]) {
+    double acc[IPL][C];
+#pragma unroll
+    for (int u = 0; u < IPL; ++u)
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[u][c] = 0.0;  // np.add.reduce identity
+    for (int m0 = 0; m0 < M; m0 += UNR) {
+        MemberLoad<DT, C, VEC> ld[IPL][UNR];
+#pragma unroll
+        for (int v = 0; v < UNR; ++v) {
+            const int m = m0 + v < M ? m0 + v : M - 1;
+#pragma unroll
+            for (int u = 0; u < IPL; ++u) ld[u][v].load(p, item_off[u] + (int64_t)m * sM, sC);
+        }
+#pragma unroll
+        for (int v = 0; v < UNR; ++v) {
+            const bool live = m0 + v < M;
+#pragma unroll
+            for (int u = 0; u < IPL; ++u) ld[u][v].add_masked(acc[u], live);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < IPL; ++u)
+#pragma unroll
+        for (int c = 0; c < C; ++c) mean[u][c] = div_members(acc[u][c], dM, invM, pow2);
+}
+
 template <int DT, int C, bool VEC, int UNR>
-__device__ __forceinline__ void committee_mean(const void* p, int64_t item_off, int M, int64_t sM,
-                                               int64_t sC, double dM, double invM, bool pow2,
-                                               double (&mean)[C]) {
-    double acc[C];
+__device__ __forceinline__ void committee_mean(const void* p, int64_t item_off, int M, int64_t sM, int64_t sC,
+                                               double dM, double invM, bool pow2, double (&mean)[C]) {
+    const int64_t offs[1] = {item_off};
+    double m1[1][C];
+    committee_mean_multi<DT, C, VEC, UNR, 1>(p, offs, M, sM, sC, dM, invM, pow2, m1);
 #pragma unroll
-    for (int c = 0; c < C; ++c) acc[c] = 0.0;  // np.add.reduce identity
-    int m = 0;
-    for (; m + UNR <= M; m += UNR) {
-        MemberLoad<DT, C, VEC> ld[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) ld[u].load(p, item_off + (int64_t)(m + u) * sM, sC);
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) ld[u].add_to(acc);
-    }
-    for (; m < M; ++m) {
-        MemberLoad<DT, C, VEC> ld;
-        ld.load(p, item_off + (int64_t)m * sM, sC);
-        ld.add_to(acc);
-    }
-#pragma unroll
-    for (int c = 0; c < C; ++c) mean[c] = div_members(acc[c], dM, invM, pow2);
+    for (int c = 0; c < C; ++c) mean[c] = m1[0][c];
 }
 
 }  // namespace ce

@@ -31,6 +31,7 @@ constexpr int kBS = 256;          // stage-1 block: 4 waves
 constexpr int kFinBS = 1024;      // stage-2 block: 16 waves
 constexpr int kMinRounds = 4;     // >= 4 rounds of kBS items per stage-1 block (batched split)
 constexpr int kMinItemsPerBlock = 64;
+constexpr int64_t kSmallPoolBytes = 256 * 1024;  // below this one block does the whole selection
 constexpr int kMaxBlocks = 1024;  // stage-1 blocks per pool (4 per CU on 256 CUs)
 
 // ---------------------------------------------------------------------------
@@ -44,8 +45,21 @@ struct CommitteeSrc {
     double dM, invM;
     bool pow2;
     static constexpr int kC = C;
+    static constexpr int kDT = DT;
+    static constexpr int kUnr = DT == kF64 ? 4 : 8;
     __device__ __forceinline__ void mean(int64_t i, double (&m)[C]) const {
-        committee_mean<DT, C, VEC, (DT == kF64 ? 4 : 8)>(p, i * sN, M, sM, sC, dM, invM, pow2, m);
+        committee_mean<DT, C, VEC, kUnr>(p, i * sN, M, sM, sC, dM, invM, pow2, m);
+    }
+    // IPL items at once: all their member loads in flight together
+    template <int UNR, int IPL>
+    __device__ __forceinline__ void keys(const int64_t (&items)[IPL], uint64_t (&k)[IPL]) const {
+        int64_t offs[IPL];
+#pragma unroll
+        for (int u = 0; u < IPL; ++u) offs[u] = items[u] * sN;
+        double m[IPL][C];
+        committee_mean_multi<DT, C, VEC, UNR, IPL>(p, offs, M, sM, sC, dM, invM, pow2, m);
+#pragma unroll
+        for (int u = 0; u < IPL; ++u) k[u] = order_key(entropy_row<C>(m[u]));
     }
     __device__ __forceinline__ double entropy(int64_t i) const {
         double m[C];
@@ -737,6 +751,19 @@ static bool stream_enabled() {
     return on;
 }
 
+// (UNR members x IPL items) loads in flight per lane for the direct paths:
+// small committees batch items, large ones batch members.
+template <class Src, class F>
+static void with_batching(int M, F&& f) {
+    if constexpr (Src::kDT == kF64 || Src::kC > 4) {
+        (void)M;
+        f(std::integral_constant<int, 4>(), std::integral_constant<int, 2>());
+    } else {
+        if (M <= 4) f(std::integral_constant<int, 4>(), std::integral_constant<int, 4>());
+        else f(std::integral_constant<int, 8>(), std::integral_constant<int, 2>());
+    }
+}
+
 // Blocks of `kernel` resident on the whole device (occupancy API x CUs), cached.
 static int device_cus() {
     static int cus[64] = {0};
@@ -804,9 +831,13 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
 #undef CE_S
     }
     int rc = with_committee(a, [&](auto src) {
-        const int grid = resident_grid(k_stream_direct<decltype(src), 2>, 0, G);
-        stream_grid(sa, grid);
-        hipLaunchKernelGGL((k_stream_direct<decltype(src), 2>), dim3(grid), dim3(256), 0, st, src, sa, q, w.c);
+        using S = decltype(src);
+        with_batching<S>(a.M, [&](auto unr, auto ipl) {
+            auto kern = k_stream_direct<S, decltype(ipl)::value, decltype(unr)::value>;
+            const int grid = resident_grid(kern, 0, G);
+            stream_grid(sa, grid);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, src, sa, q, w.c);
+        });
     });
     if (rc == CE_OK) return true;
     const WideArgs wa = wide_args(a);
@@ -962,6 +993,18 @@ extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, in
     if (!val_out || !idx_out) return fail(CE_EINVAL, "null output");
     hipStream_t st = (hipStream_t)stream;
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    if (stream_enabled() && q >= 1 && q <= kStreamMaxQ && N > 0 && val_out && idx_out &&
+        N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes && check_comm(a) == CE_OK) {
+        // small pool: one block scores and selects, one launch, no workspace traffic
+        const int rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            with_batching<S>(M, [&](auto unr, auto ipl) {
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value>), dim3(1), dim3(256),
+                                   0, st, src, nullptr, N, base_idx, q, val_out, idx_out);
+            });
+        });
+        if (rc == CE_OK) return check_launch("ce_select_mc");
+    }
     int G = 0;
     bool fin = false;
     int rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, &fin, st);
@@ -1056,8 +1099,11 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     hipStream_t st = (hipStream_t)stream;
     if (stream_enabled() && q <= kStreamMaxQ) {
         rc = with_committee(a, [&](auto src) {
-            hipLaunchKernelGGL((k_stream_seg<decltype(src), 4>), dim3(U), dim3(256), 0, st, src, offsets, q, val_out,
-                               idx_out);
+            using S = decltype(src);
+            with_batching<S>(M, [&](auto unr, auto ipl) {
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value>), dim3(U), dim3(256),
+                                   0, st, src, offsets, (int64_t)0, (int64_t)0, q, val_out, idx_out);
+            });
         });
         if (rc == CE_OK) return check_launch("ce_select_batched");
     }

@@ -273,17 +273,19 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
 // Any strides (vector loads when aligned): member-major [M, N, C] streams
 // coalesced across lanes.  IPL items per lane per iteration keep IPL x M
 // member loads in flight per lane.
-template <class Src, int IPL>
+template <class Src, int IPL, int UNR>
 __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, int64_t hi, int64_t rel, int q,
                                                     WaveTopQ<kStreamCapW>& tq) {
     const int lane = threadIdx.x & 63;
     for (int64_t t0 = lo; t0 < hi; t0 += 64 * IPL) {
         uint64_t k[IPL];
+        int64_t items[IPL];
 #pragma unroll
         for (int u = 0; u < IPL; ++u) {
             const int64_t i = t0 + 64 * u + lane;
-            k[u] = src.key(i < hi ? i : hi - 1);  // clamped: every lane loads, no branch per item
+            items[u] = i < hi ? i : hi - 1;  // clamped: every lane loads, no branch per item
         }
+        src.template keys<UNR, IPL>(items, k);
 #pragma unroll
         for (int u = 0; u < IPL; ++u) {
             const int64_t i = t0 + 64 * u + lane;
@@ -292,7 +294,7 @@ __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, 
     }
 }
 
-template <class Src, int IPL>
+template <class Src, int IPL, int UNR>
 __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, int q, Cand* __restrict__ wc) {
     __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
     __shared__ int cnt[4];
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     if (lo > hi) lo = hi;
     WaveTopQ<kStreamCapW> tq;
     tq.init(sm.key[w], sm.idx[w]);
-    stream_direct_range<Src, IPL>(src, lo, hi, a.base_idx, q, tq);
+    stream_direct_range<Src, IPL, UNR>(src, lo, hi, a.base_idx, q, tq);
     tq.flush(q);
     if (lane == 0) cnt[w] = tq.count;
     const int64_t slot = (int64_t)blockIdx.x * q;
@@ -314,13 +316,16 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
 // Batched pools (amg_test.py:345's per-user loop in one launch): block u owns
 // segment [offsets[u], offsets[u+1]), its 4 waves split it, and the block's
 // merged top-q is the user's final answer (user-local positions).
-template <class Src, int IPL>
-__global__ __launch_bounds__(256) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int q,
-                                                     double* __restrict__ oval, int64_t* __restrict__ oidx) {
+// offsets == nullptr: one segment [0, n) with positions base_idx + i (the
+// single-launch path for small pools).
+template <class Src, int IPL, int UNR>
+__global__ __launch_bounds__(256) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int64_t n,
+                                                     int64_t base_idx, int q, double* __restrict__ oval,
+                                                     int64_t* __restrict__ oidx) {
     __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
     __shared__ int cnt[4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t s0 = offsets[blockIdx.x], s1 = offsets[blockIdx.x + 1];
+    const int64_t s0 = offsets ? offsets[blockIdx.x] : 0, s1 = offsets ? offsets[blockIdx.x + 1] : n;
     const int64_t len = s1 > s0 ? s1 - s0 : 0;
     const int64_t per = ((len + 3) / 4 + 63) / 64 * 64;
     int64_t lo = s0 + w * per;
@@ -328,7 +333,7 @@ __global__ __launch_bounds__(256) void k_stream_seg(Src src, const int64_t* __re
     if (lo > hi) lo = hi;
     WaveTopQ<kStreamCapW> tq;
     tq.init(sm.key[w], sm.idx[w]);
-    stream_direct_range<Src, IPL>(src, lo, hi, -s0, q, tq);
+    stream_direct_range<Src, IPL, UNR>(src, lo, hi, (offsets ? 0 : base_idx) - s0, q, tq);
     tq.flush(q);
     if (lane == 0) cnt[w] = tq.count;
     const int64_t slot = (int64_t)blockIdx.x * q;
