@@ -44,6 +44,11 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "pool items scored+ranked/sec (M=16,C=4) at 1/2/4/8 GPUs; % HBM roofline"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+# the stage-1 kernel each layout launches at M=16, C=4, f32, q <= 64 (ce_kernels.hip launch_stream)
+STAGE1_KERNEL = {
+    "NMC": "ce::k_stream_nmc<f32, C=4, S=16> (item-major, LDS-DMA tiles)",
+    "MNC": "ce::k_stream_direct<CommitteeSrc<f32, C=4, vec>, IPL=2, UNR=8> (member-major, direct loads)",
+}
 
 
 def log(*a):
@@ -228,7 +233,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS,
                 "traffic": traffic,
-                "kernel": "k_partial<CommitteeSrc<f32,C=4,vec>> (stage 1)",
+                "kernel": STAGE1_KERNEL[args.layout],
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },

@@ -751,6 +751,16 @@ static bool stream_enabled() {
     return on;
 }
 
+// Cache policy of the item-major LDS-DMA stream: nt (default) or the default
+// policy (A/B knob CE_AMD_DMA_NT=0).
+static bool dma_nt() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_DMA_NT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // (UNR members x IPL items) loads in flight per lane for the direct paths:
 // small committees batch items, large ones batch members.
 template <class Src, class F>
@@ -821,9 +831,10 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
     if (dense_nmc && (R == 256 || R == 512)) {
 #define CE_S(DT_, C_, S_)                                                                                   \
     if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
-        const int grid = resident_grid(k_stream_nmc<DT_, C_, S_>, 0, G);                                 \
+        auto kern = dma_nt() ? k_stream_nmc<DT_, C_, S_, 2> : k_stream_nmc<DT_, C_, S_, 0>;              \
+        const int grid = resident_grid(kern, 0, G);                                                       \
         stream_grid(sa, grid);                                                                            \
-        hipLaunchKernelGGL((k_stream_nmc<DT_, C_, S_>), dim3(grid), dim3(256), 0, st, sa, q, w.c);        \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                               \
         return true;                                                                                      \
     }
         CE_S(kF32, 4, 16) CE_S(kF32, 4, 32) CE_S(kBF16, 4, 16) CE_S(kBF16, 4, 32) CE_S(kF64, 4, 32)
@@ -993,8 +1004,14 @@ extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, in
     if (!val_out || !idx_out) return fail(CE_EINVAL, "null output");
     hipStream_t st = (hipStream_t)stream;
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
-    if (stream_enabled() && q >= 1 && q <= kStreamMaxQ && N > 0 && val_out && idx_out &&
-        N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes && check_comm(a) == CE_OK) {
+    int rc0 = check_comm(a);
+    if (rc0) return rc0;
+    rc0 = check_q(q);
+    if (rc0) return rc0;
+    // the workspace contract holds on every path, even the one that does not touch it
+    if (!ws || ws_bytes < lists_bytes(pool_blocks(N), q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (stream_enabled() && q <= kStreamMaxQ && N > 0 &&
+        N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes) {
         // small pool: one block scores and selects, one launch, no workspace traffic
         const int rc = with_committee(a, [&](auto src) {
             using S = decltype(src);

@@ -107,6 +107,9 @@ struct ItemTile {
 
     // LDS-DMA the 64-row tile starting at item t0 (rows >= n_valid re-read row
     // n_valid-1, a harmless in-bounds duplicate) into `lds` (64*16*S bytes).
+    // AUX = cache-policy bits of the load (0 default, 2 = nt: the pool is
+    // streamed once, so it need not displace anything in L2 / MALL).
+    template <int AUX>
     __device__ __forceinline__ static void issue(const char* base, int64_t t0, int n_valid, char* lds) {
         const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -117,7 +120,7 @@ struct ItemTile {
             const int m = s ^ (r & 15);
             const char* src = base + (t0 + rs) * (int64_t)(16 * S) + 16 * m;
             __builtin_amdgcn_global_load_lds(
-                (const void*)src, (void __attribute__((address_space(3)))*)(lds + k * 1024), 16, 0, 0);
+                (const void*)src, (void __attribute__((address_space(3)))*)(lds + k * 1024), 16, 0, AUX);
         }
     }
 
@@ -234,8 +237,8 @@ __device__ inline void block_merge_write(uint64_t (*key)[kStreamCapW], int64_t (
     }
 }
 
-// Item-major, dense rows of 16*S bytes, LDS-DMA staged.
-template <int DT, int C, int S>
+// Item-major, dense rows of 16*S bytes, LDS-DMA staged (AUX: DMA cache policy).
+template <int DT, int C, int S, int AUX>
 __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* __restrict__ wc) {
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
     __shared__ int cnt[4];
@@ -250,14 +253,14 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     const char* base = static_cast<const char*>(a.p);
     char* lds = sm.tile[w];
     ItemTile<S> t;
-    if (lo < hi) ItemTile<S>::issue(base, lo, (int)min<int64_t>(64, hi - lo), lds);
+    if (lo < hi) ItemTile<S>::template issue<AUX>(base, lo, (int)min<int64_t>(64, hi - lo), lds);
     for (int64_t t0 = lo; t0 < hi; t0 += 64) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         t.read(lds);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         const int64_t t1 = t0 + 64;
-        if (t1 < hi) ItemTile<S>::issue(base, t1, (int)min<int64_t>(64, hi - t1), lds);
+        if (t1 < hi) ItemTile<S>::template issue<AUX>(base, t1, (int)min<int64_t>(64, hi - t1), lds);
         double mean[C];
         t.template mean<DT, C>(a.dM, a.invM, a.pow2, mean);
         const double h = entropy_row<C>(mean);

@@ -1,0 +1,53 @@
+#!/bin/bash
+# One GPU visit, in phases (each GPU step has its own limit; a fault, abort or
+# time-out ends the script -- nothing more runs on the GPU in that call).
+#   PHASE=check    pytest -m gpu, smoke(), bench.py (default line + A/B lines)
+#   PHASE=profile  rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
+# Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+LOG=$OUT/steps.log
+echo "start $PHASE $(date)" >> "$LOG"
+step() {  # $1 = status, $2 = name; 1 = test failures (keep going), anything else stops
+  echo "$2: $1" >> "$LOG"
+  case "$1" in 0|1) return 0 ;; *) echo "STOP after $2 ($1)" >> "$LOG"; exit "$1" ;; esac
+}
+bench() {  # $1 = name, rest = env/args
+  local name=$1; shift
+  timeout -k 10 300 env "$@" > "$OUT/bench_$name.json" 2> "$OUT/bench_$name.err"
+  step $? "bench $name"
+}
+case "$PHASE" in
+check)
+  timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest_gpu.log" 2>&1
+  step $? pytest
+  timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+  step $? smoke
+  bench nmc python bench.py ${BENCH_ARGS}
+  for v in ${AB}; do  # AB="name:ENV=val,ENV2=val:args ..."
+    IFS=: read -r n e a <<< "$v"
+    bench "$n" ${e//,/ } python bench.py --no-cpu-baseline ${a//\%/ }
+  done
+  ;;
+ab)  # A/B lines only: AB="name:ENV=v,ENV2=v:--arg%value ..." (% stands for a space)
+  for v in ${AB}; do
+    IFS=: read -r n e a <<< "$v"
+    bench "$n" ${e//,/ } python bench.py --no-cpu-baseline ${a//\%/ }
+  done
+  ;;
+profile)
+  LAYOUT=${LAYOUT:-NMC}
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof/trace_$LAYOUT" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --layout "$LAYOUT" > "$OUT/prof_trace_$LAYOUT.log" 2>&1
+  step $? "trace $LAYOUT"
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/fetch_$LAYOUT" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --layout "$LAYOUT" > "$OUT/prof_fetch_$LAYOUT.log" 2>&1
+  step $? "fetch $LAYOUT"
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/write_$LAYOUT" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --layout "$LAYOUT" > "$OUT/prof_write_$LAYOUT.log" 2>&1
+  step $? "write $LAYOUT"
+  ;;
+*) echo "PHASE must be check or profile" >&2; exit 2 ;;
+esac
+echo "done $PHASE $(date)" >> "$LOG"
