@@ -33,6 +33,7 @@ constexpr int kMinRounds = 4;     // >= 4 rounds of kBS items per stage-1 block 
 constexpr int kMinItemsPerBlock = 64;
 constexpr int64_t kSmallPoolBytes = 256 * 1024;  // below this one block does the whole selection
 constexpr int kMaxBlocks = 1024;  // stage-1 blocks per pool (4 per CU on 256 CUs)
+constexpr int kSegWaves = 16;     // waves per single-block pool / per user (k_stream_seg)
 
 // ---------------------------------------------------------------------------
 // Item sources.  key(i) returns the order key of global item i.
@@ -210,8 +211,7 @@ __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg
 template <int DT, int NPL, bool VEC>
 __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                      Cand* __restrict__ wc) {
-    __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
-    __shared__ int cnt[4];
+    __shared__ WaveLists sm;
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double* row = wsm + w * wide_lds_doubles(a.C);
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
     int64_t hi = lo + sa.per_wave;
     if (hi > a.N) hi = a.N;
     if (lo > hi) lo = hi;
-    WaveTopQ<kStreamCapW> tq;
-    tq.init(sm.key[w], sm.idx[w]);
+    RegTopQ tq;
+    tq.init(q);
     for (int64_t t0 = lo; t0 < hi; t0 += 64) {
         uint64_t mykey = 0;
         for (int j = 0; j < 64; ++j) {
@@ -232,12 +232,79 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
             if (lane == j) mykey = order_key(h);
         }
         const int64_t i = t0 + lane;
-        tq.offer(mykey, i + sa.base_idx, i < hi, q);
+        tq.offer(mykey, i + sa.base_idx, i < hi);
     }
-    tq.flush(q);
-    if (lane == 0) cnt[w] = tq.count;
-    const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot, sa.nlists);
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
+}
+
+// Wide classes, vectorised rows (q <= 64): one wave per item, lanes over 16-B
+// chunks, software-pipelined over the wave's flat sequence of (item, member
+// batch) pairs -- batch t+1 is in flight while batch t is added, and the next
+// item's first batch while an item's entropy is computed, so the wave always
+// has 2 x UNR x KCH 16-B loads per lane outstanding.  Items per wave are not
+// rounded to 64 (a wide item is tens of KB): every wave of the resident grid
+// gets work.
+template <int DT, int KCH, int UNR>
+__global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
+                                                      Cand* __restrict__ wc) {
+    __shared__ WaveLists sm;
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+    int64_t lo = gw * sa.per_wave;
+    int64_t hi = lo + sa.per_wave;
+    if (hi > a.N) hi = a.N;
+    if (lo > hi) lo = hi;
+    RegTopQ tq;
+    tq.init(q);
+    const char* base = static_cast<const char*>(a.p);
+    const int64_t sNb = a.sN * EB, sMb = a.sM * EB;
+    const int K = a.C / CPC;
+    const int NB = (a.M + UNR - 1) / UNR;
+    double acc[KCH * CPC];
+#pragma unroll
+    for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
+    uint64_t mykey = 0;
+    // issue cursor (item, batch) and consume cursor
+    int64_t ii = lo, ci = lo;
+    int ib = 0, cb = 0;
+    WideBatch<DT, KCH, UNR> A, B;
+    auto issue = [&](WideBatch<DT, KCH, UNR>& X) {
+        X.issue(base + ii * sNb, ib * UNR, a.M, sMb, K);
+        if (++ib == NB) {
+            ib = 0;
+            ++ii;
+        }
+    };
+    auto consume = [&](const WideBatch<DT, KCH, UNR>& X) {
+        X.add(acc, cb * UNR, a.M);
+        if (++cb == NB) {  // item ci complete
+            cb = 0;
+            const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
+#pragma unroll
+            for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
+            const int j = (int)((ci - lo) & 63);
+            if (lane == j) mykey = order_key(h);
+            if (j == 63 || ci == hi - 1) {
+                const int64_t t0 = ci - j;
+                tq.offer(mykey, t0 + lane + sa.base_idx, lane <= j);
+                mykey = 0;
+            }
+            ++ci;
+        }
+    };
+    if (ii < hi) issue(A);
+    while (ci < hi) {
+        if (ii < hi) issue(B);
+        consume(A);
+        if (ci >= hi) break;
+        if (ii < hi) issue(A);
+        consume(B);
+    }
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
 }
 
 template <int DT, int NPL, bool VEC>
@@ -445,6 +512,35 @@ __global__ __launch_bounds__(kHeadsBS) void k_finish_heads(ListSrc<FROM_VALS> sr
     write_list<2048, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
 }
 
+// Stage 2 for q <= 64: 16 waves stream the candidates (64 consecutive per wave
+// per step, PF steps in flight) through register top-q lists -- after the
+// first chunk almost nothing beats a wave's threshold -- and the 16 lists are
+// tree-merged.  No LDS buffer, no block barrier until the final merge.
+template <bool FROM_VALS>
+__global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int nl, int q,
+                                                    double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    __shared__ WaveListsT<16> sm;
+    constexpr int PF = 4;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
+    const int64_t L = (int64_t)nl * q;
+    RegTopQ tq;
+    tq.init(q);
+    for (int64_t c0 = (int64_t)w * 64; c0 < L; c0 += (int64_t)16 * 64 * PF) {
+        uint64_t k[PF];
+        int64_t id[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int64_t j = c0 + (int64_t)u * 16 * 64 + lane;
+            src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);  // clamped: no branch around a load
+            if (j >= L) id[u] = -1;
+        }
+#pragma unroll
+        for (int u = 0; u < PF; ++u) tq.offer(k[u], id[u], id[u] >= 0);
+    }
+    block_merge_write<16>(tq, sm, q, nullptr, 0, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
+}
+
 // ---------------------------------------------------------------------------
 // Per-item entropy to HBM.
 // ---------------------------------------------------------------------------
@@ -596,10 +692,23 @@ static void launch_partial(const Src& src, const Seg& sg, int grid, int q, WsLis
     }
 }
 
+// A/B knob: CE_AMD_MERGE_REG=0 -> the LDS-buffer merges (k_finish / k_finish_heads) for q <= 64 too
+static bool merge_reg_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_MERGE_REG");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <bool FROM_VALS>
 static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, double* oval, int64_t* oidx,
                           hipStream_t st) {
     const int64_t L = (int64_t)nl * q;
+    if (q <= kStreamMaxQ && merge_reg_enabled()) {
+        hipLaunchKernelGGL((k_merge_reg<FROM_VALS>), dim3(segments), dim3(1024), 0, st, src, nl, q, oval, oidx);
+        return;
+    }
     if (q <= kHeadsMaxQ && L > 256) {
         hipLaunchKernelGGL((k_finish_heads<FROM_VALS, 10>), dim3(segments), dim3(kHeadsBS), 0, st, src, nl, q, oval,
                            oidx);
@@ -761,6 +870,25 @@ static bool dma_nt() {
     return on;
 }
 
+// A/B knob: CE_AMD_WIDE2=0 -> the unpipelined wide kernel (k_stream_wide)
+static bool wide2_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_WIDE2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// A/B knob: CE_AMD_WIDE_DEEP=0 -> half the member rows per batch in k_stream_wide2
+// (fewer VGPRs, more resident waves)
+static bool wide_deep() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_WIDE_DEEP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // (UNR members x IPL items) loads in flight per lane for the direct paths:
 // small committees batch items, large ones batch members.
 template <class Src, class F>
@@ -772,6 +900,13 @@ static void with_batching(int M, F&& f) {
         if (M <= 4) f(std::integral_constant<int, 4>(), std::integral_constant<int, 4>());
         else f(std::integral_constant<int, 8>(), std::integral_constant<int, 2>());
     }
+}
+
+// The same for k_stream_seg: 16-wave blocks (<= 128 VGPRs), so fewer loads per lane.
+template <class Src, class F>
+static void with_seg_batching(F&& f) {
+    if constexpr (Src::kC > 4) f(std::integral_constant<int, 4>(), std::integral_constant<int, 1>());
+    else f(std::integral_constant<int, 4>(), std::integral_constant<int, 2>());
 }
 
 // Blocks of `kernel` resident on the whole device (occupancy API x CUs), cached.
@@ -855,7 +990,21 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
     const PwPlan pl = pw_plan(a.C);
     const size_t lds = wide_lds_bytes(a.C);
     rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
-        auto kern = k_stream_wide<decltype(dt)::value, decltype(npl)::value, decltype(vec)::value>;
+        constexpr int DT = decltype(dt)::value, NPL = decltype(npl)::value;
+        if constexpr (decltype(vec)::value) {
+            if (wide2_enabled()) {
+                constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
+                constexpr int UNR = KCH >= 8 ? 1 : 8 / KCH;
+                constexpr int UNR_LO = UNR > 1 ? UNR / 2 : 1;
+                auto kern = wide_deep() ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, UNR_LO>;
+                const int grid = resident_grid(kern, lds, G);
+                stream_grid(sa, grid);
+                sa.per_wave = cdiv(a.N, (int64_t)grid * 4);  // whole items, not 64-item tiles
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
+                return;
+            }
+        }
+        auto kern = k_stream_wide<DT, NPL, decltype(vec)::value>;
         const int grid = resident_grid(kern, lds, G);
         stream_grid(sa, grid);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
@@ -1015,8 +1164,8 @@ extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, in
         // small pool: one block scores and selects, one launch, no workspace traffic
         const int rc = with_committee(a, [&](auto src) {
             using S = decltype(src);
-            with_batching<S>(M, [&](auto unr, auto ipl) {
-                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value>), dim3(1), dim3(256),
+            with_seg_batching<S>([&](auto unr, auto ipl) {
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(1), dim3(64 * kSegWaves),
                                    0, st, src, nullptr, N, base_idx, q, val_out, idx_out);
             });
         });
@@ -1117,8 +1266,8 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     if (stream_enabled() && q <= kStreamMaxQ) {
         rc = with_committee(a, [&](auto src) {
             using S = decltype(src);
-            with_batching<S>(M, [&](auto unr, auto ipl) {
-                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value>), dim3(U), dim3(256),
+            with_seg_batching<S>([&](auto unr, auto ipl) {
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(U), dim3(64 * kSegWaves),
                                    0, st, src, offsets, (int64_t)0, (int64_t)0, q, val_out, idx_out);
             });
         });

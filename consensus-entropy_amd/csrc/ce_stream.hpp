@@ -3,8 +3,8 @@
 // One pass over the committee tensor at HBM rate.  Every wave is independent
 // while streaming (no block barriers in the loop): it owns a contiguous run of
 // 64-item tiles, scores one item per lane, and keeps its own top-q candidates
-// in a private LDS buffer (WaveTopQ).  The block's four wave lists are merged
-// once at the end.
+// in registers (RegTopQ, one list slot per lane).  The block's four wave
+// lists are merged once at the end.
 //
 // Item-major [N, M, C] tensors (each item's M*C values contiguous, R bytes)
 // are staged through LDS: a wave's 64 x R-byte tile arrives by LDS-DMA
@@ -24,77 +24,128 @@
 namespace ce {
 
 // ---------------------------------------------------------------------------
-// Per-wave top-q: a CAPW-entry LDS buffer, threshold in (wave-uniform) regs.
+// Per-wave top-q held in registers (q <= 64): lane L holds the L-th best
+// (order key, position) of the wave so far, best first; empty slots hold the
+// sentinel (0, INT64_MAX), worse than every real candidate (no finite, inf or
+// NaN entropy maps to key 0).  The threshold is slot q-1, read into scalar
+// registers.  A candidate that beats it is rare once the stream is warm: one
+// or a few are inserted in place (ballot for the position + one lane shift);
+// a large batch (the first tiles) is bitonic-sorted across the wave and
+// merged with the list -- shuffles only, no LDS, no barrier.
 // ---------------------------------------------------------------------------
-template <int CAPW>
-struct WaveTopQ {
-    uint64_t* key;
-    int64_t* idx;
-    int count;
-    uint64_t tkey;
-    int64_t tidx;
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
 
-    __device__ __forceinline__ void init(uint64_t* k, int64_t* i) {
-        key = k;
-        idx = i;
-        count = 0;
-        tkey = 0;
-        tidx = INT64_MAX;
+// (k, i) from lane `src` (per-lane index) -- ds_bpermute on the four halves
+__device__ __forceinline__ void shfl_cand(uint64_t& k, int64_t& i, int src) {
+    const int a = src << 2;
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)k);
+    const uint32_t k1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(k >> 32));
+    const uint32_t i0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(uint64_t)i);
+    const uint32_t i1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)((uint64_t)i >> 32));
+    k = ((uint64_t)k1 << 32) | k0;
+    i = (int64_t)(((uint64_t)i1 << 32) | i0);
+}
+
+// One compare-exchange stage of a bitonic network across the wave: partner
+// lane ^ j; `desc` = this lane's block sorts best-first.
+__device__ __forceinline__ void cx_stage(uint64_t& k, int64_t& i, int j, bool desc) {
+    const int lane = threadIdx.x & 63;
+    uint64_t pk = k;
+    int64_t pi = i;
+    shfl_cand(pk, pi, lane ^ j);
+    const bool lower = (lane & j) == 0;
+    const bool pb = better(pk, pi, k, i);
+    const bool take = (lower == desc) ? pb : !pb;
+    if (take) {
+        k = pk;
+        i = pi;
+    }
+}
+
+// Sort the wave's 64 (k, i) best-first.
+__device__ __forceinline__ void wave_sort64(uint64_t& k, int64_t& i) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = 2; s <= 64; s <<= 1)
+#pragma unroll
+        for (int j = s >> 1; j > 0; j >>= 1) cx_stage(k, i, j, (lane & s) == 0);
+}
+
+// (k, i) := best 64 of the two best-first lists (k, i) and (bk, bi), best-first.
+__device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t bk, int64_t bi) {
+    const int lane = threadIdx.x & 63;
+    shfl_cand(bk, bi, 63 - lane);  // reversed: list max(A[L], B[63-L]) is bitonic
+    if (better(bk, bi, k, i)) {
+        k = bk;
+        i = bi;
+    }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) cx_stage(k, i, j, true);
+}
+
+struct RegTopQ {
+    uint64_t k;   // this lane's slot
+    int64_t i;
+    uint64_t tk;  // threshold = slot q-1 (wave-uniform)
+    int64_t ti;
+    int q;
+
+    __device__ __forceinline__ void init(int q_) {
+        k = 0;
+        i = INT64_MAX;
+        tk = 0;
+        ti = INT64_MAX;
+        q = q_;
     }
 
-    // bitonic sort of [0, n) best-first (wave-synchronous: a single wave's LDS
-    // operations execute in program order, so no barrier is needed)
-    __device__ void sort(int n) {
+    __device__ __forceinline__ void refresh() {
+        tk = readlane64(k, q - 1);
+        ti = (int64_t)readlane64((uint64_t)i, q - 1);
+    }
+
+    // insert one wave-uniform candidate that beats the threshold
+    __device__ __forceinline__ void insert(uint64_t ck, int64_t ci) {
         const int lane = threadIdx.x & 63;
-        int P = 1;
-        while (P < n) P <<= 1;
-        for (int t = n + lane; t < P; t += 64) {
-            key[t] = 0;
-            idx[t] = INT64_MAX;
+        const uint64_t below = __ballot(better(ck, ci, k, i));  // slots the candidate beats: a suffix
+        const int p = __builtin_ctzll(below);
+        uint64_t uk = k;
+        int64_t ui = i;
+        shfl_cand(uk, ui, lane > 0 ? lane - 1 : 0);
+        if (lane > p) {
+            k = uk;
+            i = ui;
+        } else if (lane == p) {
+            k = ck;
+            i = ci;
         }
-        __builtin_amdgcn_wave_barrier();
-        for (int k = 2; k <= P; k <<= 1) {
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int t = lane; t < (P >> 1); t += 64) {
-                    const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-                    const int l = i + j;
-                    const bool desc = (i & k) == 0;
-                    const uint64_t ki = key[i], kl = key[l];
-                    const int64_t ii = idx[i], il = idx[l];
-                    if (better(kl, il, ki, ii) == desc) {
-                        key[i] = kl;
-                        key[l] = ki;
-                        idx[i] = il;
-                        idx[l] = ii;
-                    }
+    }
+
+    __device__ __forceinline__ void offer(uint64_t ck, int64_t ci, bool valid) {
+        const bool pass = valid && better(ck, ci, tk, ti);
+        uint64_t mask = __ballot(pass);
+        if (mask == 0) return;  // wave-uniform: the common case
+        if (__popcll(mask) <= 8) {
+            do {
+                const int s = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const uint64_t sk = readlane64(ck, s);
+                const int64_t si = (int64_t)readlane64((uint64_t)ci, s);
+                if (better(sk, si, tk, ti)) {  // re-check: earlier inserts raised the bar
+                    insert(sk, si);
+                    refresh();
                 }
-                __builtin_amdgcn_wave_barrier();
-            }
+            } while (mask);
+        } else {
+            uint64_t bk = pass ? ck : 0ull;
+            int64_t bi = pass ? ci : INT64_MAX;
+            wave_sort64(bk, bi);
+            wave_merge64(k, i, bk, bi);
+            refresh();
         }
-    }
-
-    __device__ void flush(int q) {
-        const int n = count;
-        sort(n);
-        count = n < q ? n : q;
-        if (n >= q) {
-            tkey = key[q - 1];
-            tidx = idx[q - 1];
-        }
-    }
-
-    __device__ __forceinline__ void offer(uint64_t k, int64_t i, bool valid, int q) {
-        const bool pass = valid && better(k, i, tkey, tidx);
-        const uint64_t mask = __ballot(pass);
-        if (mask == 0) return;
-        if (pass) {
-            const int pos = count + mbcnt(mask);
-            key[pos] = k;
-            idx[pos] = i;
-        }
-        __builtin_amdgcn_wave_barrier();
-        count += __popcll(mask);
-        if (count > CAPW - 64) flush(q);
     }
 };
 
@@ -166,19 +217,20 @@ struct ItemTile {
     }
 };
 
-constexpr int kStreamCapW = 128;  // per-wave candidate buffer: q <= 64
-constexpr int kStreamMaxQ = kStreamCapW - 64;
+constexpr int kStreamMaxQ = 64;  // one list slot per lane
+
+// block-merge scratch: the wave lists, 64 slots each
+template <int WAVES>
+struct WaveListsT {
+    uint64_t key[WAVES][64];
+    int64_t idx[WAVES][64];
+};
+using WaveLists = WaveListsT<4>;
 
 template <int S>
 struct StreamSmemNMC {
     char tile[4][64 * 16 * S];  // one staging tile per wave
-    uint64_t key[4][kStreamCapW];
-    int64_t idx[4][kStreamCapW];
-};
-
-struct StreamSmemDirect {
-    uint64_t key[4][kStreamCapW];
-    int64_t idx[4][kStreamCapW];
+    WaveLists lists;
 };
 
 struct StreamArgs {
@@ -193,46 +245,37 @@ struct StreamArgs {
     int nlists;        // workspace lists (>= gridDim.x); lists past the grid are written empty
 };
 
-// Merge the block's 4 wave lists (each best-first, <= q entries, counts in
-// cnt[]) into the block's top-q and write it to the workspace.  Wave 0 does it
-// in LDS scratch that held the wave buffers.
-__device__ inline void block_merge_write(uint64_t (*key)[kStreamCapW], int64_t (*idx)[kStreamCapW], int* cnt,
-                                         int q, Cand* wc, int nlists, double* oval = nullptr,
-                                         int64_t* oidx = nullptr) {
+// Merge the block's WAVES wave lists (registers, best-first) into the
+// block's top-q and write it: to the workspace (wc) or as final (val, idx)
+// outputs.  A tree over the waves: at level s, waves w = s mod 2s park their
+// list in LDS and waves w = 0 mod 2s merge it in (7 shuffle stages); every
+// LDS slot is written once and read once, one barrier per level.
+template <int WAVES>
+__device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L, int q, Cand* wc, int nlists,
+                                         double* oval = nullptr, int64_t* oidx = nullptr) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // empty lists for the workspace slots no block of this (occupancy-sized)
     // grid owns: b + gridDim.x, b + 2*gridDim.x, ...
     for (int64_t s = (int64_t)blockIdx.x + gridDim.x; s < nlists; s += gridDim.x)
         for (int r = threadIdx.x; r < q; r += blockDim.x) wc[(s - blockIdx.x) * q + r] = Cand{0ull, -1};
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        // gather wave 1..3 lists behind wave 0's (wave 0's buffer has room:
-        // 4 * q <= 256 entries are staged in the two first rows of key/idx)
-        uint64_t* mk = &key[0][0];
-        int64_t* mi = &idx[0][0];
-        int n = cnt[0];
-        // key[0..3] rows are contiguous: [4][128] -> 512 entries of scratch
-        for (int w = 1; w < 4; ++w) {
-            for (int r = lane; r < cnt[w]; r += 64) {
-                mk[n + r] = key[w][r];
-                mi[n + r] = idx[w][r];
-            }
-            n += cnt[w];
-            __builtin_amdgcn_wave_barrier();
+    uint64_t k = tq.k;
+    int64_t i = tq.i;
+#pragma unroll
+    for (int s = 1; s < WAVES; s <<= 1) {
+        if ((w & (2 * s - 1)) == s) {
+            L.key[w][lane] = k;
+            L.idx[w][lane] = i;
         }
-        WaveTopQ<4 * kStreamCapW> wq;
-        wq.init(mk, mi);
-        wq.count = n;
-        wq.sort(n);
-        __builtin_amdgcn_wave_barrier();
-        for (int r = lane; r < q; r += 64) {
-            const bool ok = r < n;
-            if (oval) {
-                oval[r] = ok ? key_to_val(mk[r]) : __longlong_as_double(0x7ff8000000000000ll);
-                oidx[r] = ok ? mi[r] : -1;
-            } else {
-                wc[r] = Cand{ok ? mk[r] : 0ull, ok ? mi[r] : -1};
-            }
+        __syncthreads();
+        if ((w & (2 * s - 1)) == 0) wave_merge64(k, i, L.key[w + s][lane], L.idx[w + s][lane]);
+    }
+    if (w == 0 && lane < q) {
+        const bool ok = i != INT64_MAX;
+        if (oval) {
+            oval[lane] = ok ? key_to_val(k) : __longlong_as_double(0x7ff8000000000000ll);
+            oidx[lane] = ok ? i : -1;
+        } else {
+            wc[lane] = Cand{ok ? k : 0ull, ok ? i : -1};
         }
     }
 }
@@ -241,15 +284,14 @@ __device__ inline void block_merge_write(uint64_t (*key)[kStreamCapW], int64_t (
 template <int DT, int C, int S, int AUX>
 __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* __restrict__ wc) {
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
-    __shared__ int cnt[4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
     int64_t lo = gw * a.per_wave;
     int64_t hi = lo + a.per_wave;
     if (hi > a.N) hi = a.N;
     if (lo > hi) lo = hi;
-    WaveTopQ<kStreamCapW> tq;
-    tq.init(sm.key[w], sm.idx[w]);
+    RegTopQ tq;
+    tq.init(q);
     const char* base = static_cast<const char*>(a.p);
     char* lds = sm.tile[w];
     ItemTile<S> t;
@@ -265,12 +307,9 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
         t.template mean<DT, C>(a.dM, a.invM, a.pow2, mean);
         const double h = entropy_row<C>(mean);
         const int64_t i = t0 + lane;
-        tq.offer(order_key(h), i + a.base_idx, i < hi, q);
+        tq.offer(order_key(h), i + a.base_idx, i < hi);
     }
-    tq.flush(q);
-    if (lane == 0) cnt[w] = tq.count;
-    const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot, a.nlists);
+    block_merge_write<4>(tq, sm.lists, q, wc + (int64_t)blockIdx.x * q, a.nlists);
 }
 
 // Any strides (vector loads when aligned): member-major [M, N, C] streams
@@ -278,7 +317,7 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
 // member loads in flight per lane.
 template <class Src, int IPL, int UNR>
 __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, int64_t hi, int64_t rel, int q,
-                                                    WaveTopQ<kStreamCapW>& tq) {
+                                                    RegTopQ& tq) {
     const int lane = threadIdx.x & 63;
     for (int64_t t0 = lo; t0 < hi; t0 += 64 * IPL) {
         uint64_t k[IPL];
@@ -292,55 +331,49 @@ __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, 
 #pragma unroll
         for (int u = 0; u < IPL; ++u) {
             const int64_t i = t0 + 64 * u + lane;
-            tq.offer(k[u], i + rel, i < hi, q);
+            tq.offer(k[u], i + rel, i < hi);
         }
     }
 }
 
 template <class Src, int IPL, int UNR>
 __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, int q, Cand* __restrict__ wc) {
-    __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
-    __shared__ int cnt[4];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ WaveLists sm;
+    const int w = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
     int64_t lo = gw * a.per_wave;
     int64_t hi = lo + a.per_wave;
     if (hi > a.N) hi = a.N;
     if (lo > hi) lo = hi;
-    WaveTopQ<kStreamCapW> tq;
-    tq.init(sm.key[w], sm.idx[w]);
+    RegTopQ tq;
+    tq.init(q);
     stream_direct_range<Src, IPL, UNR>(src, lo, hi, a.base_idx, q, tq);
-    tq.flush(q);
-    if (lane == 0) cnt[w] = tq.count;
-    const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, wc + slot, a.nlists);
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists);
 }
 
 // Batched pools (amg_test.py:345's per-user loop in one launch): block u owns
-// segment [offsets[u], offsets[u+1]), its 4 waves split it, and the block's
-// merged top-q is the user's final answer (user-local positions).
-// offsets == nullptr: one segment [0, n) with positions base_idx + i (the
-// single-launch path for small pools).
-template <class Src, int IPL, int UNR>
-__global__ __launch_bounds__(256) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int64_t n,
-                                                     int64_t base_idx, int q, double* __restrict__ oval,
-                                                     int64_t* __restrict__ oidx) {
-    __shared__ __attribute__((aligned(16))) StreamSmemDirect sm;
-    __shared__ int cnt[4];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// segment [offsets[u], offsets[u+1]), its WAVES waves split it in whole
+// iterations of 64*IPL items, and the block's merged top-q is the user's final
+// answer (user-local positions).  offsets == nullptr: one segment [0, n) with
+// positions base_idx + i (the single-launch path for small pools).
+template <class Src, int IPL, int UNR, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int64_t n,
+                                                            int64_t base_idx, int q, double* __restrict__ oval,
+                                                            int64_t* __restrict__ oidx) {
+    __shared__ WaveListsT<WAVES> sm;
+    const int w = threadIdx.x >> 6;
     const int64_t s0 = offsets ? offsets[blockIdx.x] : 0, s1 = offsets ? offsets[blockIdx.x + 1] : n;
     const int64_t len = s1 > s0 ? s1 - s0 : 0;
-    const int64_t per = ((len + 3) / 4 + 63) / 64 * 64;
+    constexpr int64_t kIt = 64 * IPL;
+    const int64_t per = ((len + kIt - 1) / kIt + WAVES - 1) / WAVES * kIt;
     int64_t lo = s0 + w * per;
     int64_t hi = lo + per < s1 ? lo + per : s1;
     if (lo > hi) lo = hi;
-    WaveTopQ<kStreamCapW> tq;
-    tq.init(sm.key[w], sm.idx[w]);
+    RegTopQ tq;
+    tq.init(q);
     stream_direct_range<Src, IPL, UNR>(src, lo, hi, (offsets ? 0 : base_idx) - s0, q, tq);
-    tq.flush(q);
-    if (lane == 0) cnt[w] = tq.count;
     const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write(sm.key, sm.idx, cnt, q, nullptr, 0, oval + slot, oidx + slot);
+    block_merge_write<WAVES>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot);
 }
 
 }  // namespace ce

@@ -202,6 +202,55 @@ __device__ __forceinline__ void chunk_add(const uint32_t (&u)[4], double* acc) {
     }
 }
 
+template <int DT>
+__device__ __forceinline__ void chunk_add_masked(const uint32_t (&u)[4], double* acc, bool live) {
+    if constexpr (DT == kF32) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += live ? (double)__uint_as_float(u[e]) : 0.0;
+    } else if constexpr (DT == kF64) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            acc[e] += live ? __longlong_as_double((long long)(((uint64_t)u[2 * e + 1] << 32) | u[2 * e])) : 0.0;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += live ? bf16_to_f64((u[e >> 1] >> (16 * (e & 1))) & 0xffffu) : 0.0;
+    }
+}
+
+// scipy.stats.entropy of the consensus row whose member sums sit in this
+// wave's registers (lane l: chunks l, l+64, ... of CPC classes each), via the
+// per-wave LDS row: mean = acc / M, row sum, entr, row sum (amg_test.py:441-443).
+template <int DT, int KCH>
+__device__ __forceinline__ double wave_entropy_from_sums(double* acc, int K, double dM, double invM, bool pow2,
+                                                        const PwPlan& pl, double* row, double* scratch) {
+    // acc is overwritten with the mean row (its last use), saving KCH*CPC registers
+    constexpr int CPC = ChunkT<DT>::CPC;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int kk = 0; kk < KCH; ++kk) {
+        const int ch = lane + 64 * kk;
+#pragma unroll
+        for (int e = 0; e < CPC; ++e) {
+            acc[kk * CPC + e] = div_members(acc[kk * CPC + e], dM, invM, pow2);
+            if (ch < K) row[ch * CPC + e] = acc[kk * CPC + e];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double s = wave_row_sum(row, pl, scratch);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kk = 0; kk < KCH; ++kk) {
+        const int ch = lane + 64 * kk;
+#pragma unroll
+        for (int e = 0; e < CPC; ++e)
+            if (ch < K) row[ch * CPC + e] = entr(1.0 * acc[kk * CPC + e] / s);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double h = wave_row_sum(row, pl, scratch);
+    __builtin_amdgcn_wave_barrier();
+    return h;
+}
+
 template <int DT, int KCH, int UNR>
 __device__ inline double wave_item_entropy_vec(const void* p, int64_t off, int M, int C, int64_t sM, double dM,
                                                double invM, bool pow2, const PwPlan& pl, double* row,
@@ -246,30 +295,45 @@ __device__ inline double wave_item_entropy_vec(const void* p, int64_t off, int M
             chunk_add<DT>(t, acc + kk * CPC);
         }
     }
+    return wave_entropy_from_sums<DT, KCH>(acc, K, dM, invM, pow2, pl, row, scratch);
+}
+
+// One batch of UNR member rows x KCH 16-B chunks per lane of one item (raw
+// words, no conversion until the adds).  Members past M re-load member M-1
+// (in bounds) and are added as +0.0 (bit-exact no-op, see committee_mean_multi).
+template <int DT, int KCH, int UNR>
+struct WideBatch {
+    uint32_t v[UNR][KCH][4];
+
+    __device__ __forceinline__ void issue(const char* item, int m0, int M, int64_t sMb, int K) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int kk = 0; kk < KCH; ++kk) {
-        const int ch = lane + 64 * kk;
+        for (int u = 0; u < UNR; ++u) {
+            const int m = m0 + u < M ? m0 + u : M - 1;
 #pragma unroll
-        for (int e = 0; e < CPC; ++e) {
-            acc[kk * CPC + e] = div_members(acc[kk * CPC + e], dM, invM, pow2);
-            if (ch < K) row[ch * CPC + e] = acc[kk * CPC + e];
+            for (int kk = 0; kk < KCH; ++kk) {
+                const int ch = lane + 64 * kk;
+                const int chs = ch < K ? ch : K - 1;
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(item + (int64_t)m * sMb) + chs);
+                v[u][kk][0] = x.x;
+                v[u][kk][1] = x.y;
+                v[u][kk][2] = x.z;
+                v[u][kk][3] = x.w;
+            }
         }
     }
-    __builtin_amdgcn_wave_barrier();
-    const double s = wave_row_sum(row, pl, scratch);
-    __builtin_amdgcn_wave_barrier();
+
+    __device__ __forceinline__ void add(double* acc, int m0, int M) const {
+        constexpr int CPC = ChunkT<DT>::CPC;
 #pragma unroll
-    for (int kk = 0; kk < KCH; ++kk) {
-        const int ch = lane + 64 * kk;
+        for (int u = 0; u < UNR; ++u) {
+            const bool live = m0 + u < M;
 #pragma unroll
-        for (int e = 0; e < CPC; ++e)
-            if (ch < K) row[ch * CPC + e] = entr(1.0 * acc[kk * CPC + e] / s);
+            for (int kk = 0; kk < KCH; ++kk) chunk_add_masked<DT>(v[u][kk], acc + kk * CPC, live);
+        }
     }
-    __builtin_amdgcn_wave_barrier();
-    const double h = wave_row_sum(row, pl, scratch);
-    __builtin_amdgcn_wave_barrier();
-    return h;
-}
+};
 
 struct WideArgs {
     const void* p;

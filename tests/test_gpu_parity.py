@@ -252,3 +252,91 @@ def test_full_size_property(ce):
     assert beat + tie_lower == q - 1
     del P, ent
     torch.cuda.empty_cache()
+
+
+def _bf16_bits(P32):
+    """float32 -> bf16 bit patterns (round to nearest even), as uint16."""
+    u = P32.astype(np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return u.astype(np.uint16)
+
+
+@pytest.mark.parametrize("N,M,C,dt", [(5_000, 32, 1000, "bf16"), (3_001, 5, 1000, "bf16"),
+                                      (2_000, 7, 1000, "f32"), (1_500, 3, 2048, "f64"),
+                                      (4_000, 9, 136, "bf16")])
+def test_wide_stream_vs_oracle(ce, N, M, C, dt):
+    """The pipelined wide-class stream (one wave per item, member batches past M
+    masked) against the oracle, item-major and member-major, several waves'
+    worth of items each."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(N + M + C)
+    P = synth(rng, N, M, C, np.float32)
+    if dt == "bf16":
+        host = _bf16_bits(P)
+        Pd = dev(host.view(np.int16)).view(torch.bfloat16)
+    else:
+        host = P.astype(np.float64) if dt == "f64" else P
+        Pd = dev(host)
+    ent_o = O.oracle_committee_entropy(host, "NMC")
+    for q in (10, 64):
+        _, idx_o = O.oracle_topq(ent_o, q)
+        _, idx = ce.ops.select_mc(Pd, q, "NMC")
+        assert np.array_equal(idx_np(idx), idx_o), (q, "NMC")
+    _, idx = ce.ops.select_mc(Pd.permute(1, 0, 2).contiguous(), 10, "MNC")
+    assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
+
+
+@pytest.mark.parametrize("sizes", [[1608] * 37, [1, 64, 65, 0, 5000, 127, 20000, 3], [100_000, 70_000]])
+def test_batched_segments_vs_oracle(ce, sizes):
+    """Per-user selection in one launch (16-wave blocks, one per user): ragged
+    users, an empty user, users of 1 item and users spanning many iterations."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(len(sizes))
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    P = synth(rng, int(offs[-1]), 4, 4, np.float32, quant=16)  # quantised: many exact ties
+    Pm = np.ascontiguousarray(np.transpose(P, (1, 0, 2)))
+    ent_o = O.oracle_committee_entropy(P, "NMC")
+    _, idx = ce.ops.select_batched(dev(Pm), dev(offs), 10, "MNC")
+    idx = idx.cpu().numpy()
+    for u in range(len(sizes)):
+        io = O.oracle_topq(ent_o[offs[u]:offs[u + 1]], 10)[1]
+        got = idx[u][idx[u] >= 0]
+        assert np.array_equal(got, io), u
+
+
+@pytest.mark.parametrize("nl,q", [(1, 10), (3, 1), (64, 10), (1024, 10), (1024, 64), (5000, 17)])
+def test_merge_lists_vs_oracle(ce, nl, q):
+    """Stage-2 merge (register lists, 16 waves) over many best-first lists,
+    with ties across lists, NaN, empty tails and whole empty lists."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(nl * 100 + q)
+    vals = np.round(rng.random((nl, q)), 2)  # coarse: many equal keys
+    vals[rng.random((nl, q)) < 0.001] = np.nan
+    idx = rng.permutation(nl * q * 3)[: nl * q].reshape(nl, q).astype(np.int64)
+    for r in range(nl):
+        key = np.where(np.isnan(vals[r]), np.inf, vals[r])
+        o = np.lexsort((idx[r], -key))
+        vals[r], idx[r] = vals[r][o], idx[r][o]
+    cut = rng.integers(0, q + 1, nl)
+    for r in range(nl):
+        if rng.random() < 0.2:
+            idx[r, cut[r]:] = -1
+            vals[r, cut[r]:] = np.nan
+    v, i = ce.ops.topq_merge(dev(vals.ravel()), dev(idx.ravel()), q)
+    vo, io = O.oracle_topq_merge(vals.ravel(), idx.ravel(), q)
+    assert np.array_equal(idx_np(i), io)
+
+
+@pytest.mark.parametrize("N", [1, 63, 64, 65, 1608, 4096, 16384])
+def test_small_pool_single_launch(ce, N):
+    """Pools under kSmallPoolBytes: one 16-wave block scores and selects."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(N)
+    P = synth(rng, N, 4, 4, np.float32, quant=8)
+    for q in (1, 10, 64):
+        _, idx = ce.ops.select_mc(dev(np.transpose(P, (1, 0, 2))), q, "MNC")
+        assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, q, "NMC")[1]), q

@@ -21,30 +21,35 @@ import ce_amd.ops as ops  # noqa: E402
 PEAK = 8000.0
 
 
-def timed(fn, reps, graph=True):
-    """Seconds per call.  graph=True: one call captured in a HIP graph and
-    replayed, so Python/ctypes launch overhead is excluded (device time of the
-    call's kernels and the gaps between them)."""
+def timed(fn, reps, graph=True, per_graph=20):
+    """Seconds per call.  graph=True: `per_graph` back-to-back calls captured
+    in one HIP graph and replayed, so Python/ctypes launch overhead and the
+    graph-launch cost (~10 us per replay) are amortised: the figure is device
+    time of the call's kernels plus the gaps between them."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
     if graph:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            fn()
+            for _ in range(per_graph):
+                fn()
         run = g.replay
+        n_run = max(1, reps // per_graph)
+        calls = n_run * per_graph
     else:
         run = fn
-    for _ in range(3):
+        n_run = calls = reps
+    for _ in range(2):
         run()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
+    for _ in range(n_run):
         run()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps * 1e-3
+    return a.elapsed_time(b) / calls * 1e-3
 
 
 def dirichlet(shape, dtype=torch.float32, gen=None):
