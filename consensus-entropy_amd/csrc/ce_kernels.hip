@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     const char* base = static_cast<const char*>(a.p);
     const int64_t sNb = a.sN * EB, sMb = a.sM * EB;
     const int K = a.C / CPC;
-    const int NB = (a.M + UNR - 1) / UNR;
+    const int NB = a.M / UNR;  // UNR divides M (host)
     double acc[KCH * CPC];
 #pragma unroll
     for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
@@ -273,14 +273,14 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     int ib = 0, cb = 0;
     WideBatch<DT, KCH, UNR> A, B;
     auto issue = [&](WideBatch<DT, KCH, UNR>& X) {
-        X.issue(base + ii * sNb, ib * UNR, a.M, sMb, K);
+        X.issue(base + ii * sNb, ib * UNR, sMb, K);
         if (++ib == NB) {
             ib = 0;
             ++ii;
         }
     };
     auto consume = [&](const WideBatch<DT, KCH, UNR>& X) {
-        X.add(acc, cb * UNR, a.M);
+        X.add(acc);
         if (++cb == NB) {  // item ci complete
             cb = 0;
             const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
@@ -879,16 +879,6 @@ static bool wide2_enabled() {
     return on;
 }
 
-// A/B knob: CE_AMD_WIDE_DEEP=0 -> half the member rows per batch in k_stream_wide2
-// (fewer VGPRs, more resident waves)
-static bool wide_deep() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_WIDE_DEEP");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 // (UNR members x IPL items) loads in flight per lane for the direct paths:
 // small committees batch items, large ones batch members.
 template <class Src, class F>
@@ -994,9 +984,9 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
         if constexpr (decltype(vec)::value) {
             if (wide2_enabled()) {
                 constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
-                constexpr int UNR = KCH >= 8 ? 1 : 8 / KCH;
-                constexpr int UNR_LO = UNR > 1 ? UNR / 2 : 1;
-                auto kern = wide_deep() ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, UNR_LO>;
+                // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
+                constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
+                auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
                 const int grid = resident_grid(kern, lds, G);
                 stream_grid(sa, grid);
                 sa.per_wave = cdiv(a.N, (int64_t)grid * 4);  // whole items, not 64-item tiles

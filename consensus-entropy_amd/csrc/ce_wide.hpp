@@ -4,9 +4,10 @@
 // The row sums inside scipy.stats.entropy use numpy's pairwise summation
 // (leaves of <= 128 elements summed with 8 strided accumulators, combined by a
 // fixed binary tree).  The host builds the tree for the call's C once
-// (PwPlan: leaves + postfix combine program); each leaf is summed by 8 lanes
-// with shuffles reproducing ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), and lane 0
-// runs the combine program -- the same additions in the same order as numpy.
+// (PwPlan: leaves + the internal nodes as rounds of lane pairs); each leaf is
+// summed by 8 lanes with shuffles reproducing ((r0+r1)+(r2+r3))+((r4+r5)+
+// (r6+r7)), and the tree is combined by shuffles -- the same additions in the
+// same order as numpy.
 #pragma once
 #include "ce_device.hpp"
 #include "ce_topq.hpp"
@@ -14,54 +15,69 @@
 namespace ce {
 
 constexpr int kWideMaxC = 2048;
-constexpr int kPwMaxLeaves = 32;
+constexpr int kPwMaxLeaves = 32;  // leaves hold 64..128 elements when n > 128: <= 32 for n <= 2048
+constexpr int kPwMaxRounds = 6;   // tree height (<= 5 for n <= 2048)
 
+// numpy's pairwise-summation tree for one n: the leaves (start, length) in
+// order, and the internal nodes as rounds of lane pairs.  Every subtree's sum
+// lives in the lane of its leftmost leaf; a node of height h is evaluated in
+// round h-1 as lane[a] = lane[a] + lane[b] (a = its left child's leftmost
+// leaf, b = its right child's), so the left operand stays on the left.
 struct PwPlan {
     int n;
     int nleaves;
-    int nops;
+    int nrounds;
     short lstart[kPwMaxLeaves];
     short llen[kPwMaxLeaves];
-    signed char ops[2 * kPwMaxLeaves];  // >= 0: push leaf; -1: pop two, push sum
+    signed char partner[kPwMaxRounds][kPwMaxLeaves];  // round r: lane a adds lane partner[r][a]; -1 none
 };
 
-// Host: numpy's recursion (loops_utils.h.src) for n elements.
-static inline void pw_build(PwPlan& pl, int start, int n) {
+// Host: numpy's recursion (loops_utils.h.src) for n elements.  Returns the
+// subtree height; *first = its leftmost leaf.
+static inline int pw_build(PwPlan& pl, int start, int n, int* first) {
     if (n <= 128) {
+        *first = pl.nleaves;
         pl.lstart[pl.nleaves] = (short)start;
         pl.llen[pl.nleaves] = (short)n;
-        pl.ops[pl.nops++] = (signed char)pl.nleaves;
         pl.nleaves++;
-        return;
+        return 0;
     }
     int n2 = n / 2;
     n2 -= n2 % 8;
-    pw_build(pl, start, n2);
-    pw_build(pl, start + n2, n - n2);
-    pl.ops[pl.nops++] = -1;
+    int a = 0, b = 0;
+    const int ha = pw_build(pl, start, n2, &a);
+    const int hb = pw_build(pl, start + n2, n - n2, &b);
+    const int h = 1 + (ha > hb ? ha : hb);
+    pl.partner[h - 1][a] = (signed char)b;
+    if (h > pl.nrounds) pl.nrounds = h;
+    *first = a;
+    return h;
 }
 
 static inline PwPlan pw_plan(int n) {
     PwPlan pl{};
     pl.n = n;
-    if (n >= 8) pw_build(pl, 0, n);
+    for (int r = 0; r < kPwMaxRounds; ++r)
+        for (int l = 0; l < kPwMaxLeaves; ++l) pl.partner[r][l] = -1;
+    int first = 0;
+    if (n >= 8) pw_build(pl, 0, n, &first);
     return pl;
 }
 
 // Wave-cooperative np.sum(a[0:n]) over an LDS row (returns the same value in
-// every lane).  scratch: >= kPwMaxLeaves + 8 doubles of per-wave LDS.
+// every lane): each leaf is summed by 8 lanes with numpy's 8 strided
+// accumulators and ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), leaf l's sum moves
+// to lane l, and the tree is combined in pl.nrounds shuffle rounds -- the same
+// additions in the same order as numpy, no serial lane-0 section.
 __device__ inline double wave_row_sum(const double* a, const PwPlan& pl, double* scratch) {
+    (void)scratch;
     const int lane = threadIdx.x & 63;
-    double res = 0.0;
     if (pl.n < 8) {
-        if (lane == 0) {
-            double r = -0.0;
-            for (int i = 0; i < pl.n; ++i) r += a[i];
-            res = 0.0 + r;
-        }
-        return __shfl(res, 0);
+        double r = -0.0;
+        for (int i = 0; i < pl.n; ++i) r += a[i];
+        return 0.0 + r;  // every lane computes it (LDS broadcast reads)
     }
-    // leaves: 8 lanes per leaf, 8 leaves per pass
+    double lv = 0.0;  // lane l < nleaves: leaf l's (then its subtree's) sum
     for (int l0 = 0; l0 < pl.nleaves; l0 += 8) {
         const int leaf = l0 + (lane >> 3), j = lane & 7;
         double r = 0.0;
@@ -76,29 +92,17 @@ __device__ inline double wave_row_sum(const double* a, const PwPlan& pl, double*
         r = r + __shfl_xor(r, 1);
         r = r + __shfl_xor(r, 2);
         r = r + __shfl_xor(r, 4);
-        if (leaf < pl.nleaves && j == 0) {
+        if (leaf < pl.nleaves && j == 0)
             for (int i = len - (len % 8); i < len; ++i) r += a[st + i];
-            scratch[leaf] = r;
-        }
+        const double t = __shfl(r, ((lane - l0) & 7) << 3);
+        if (lane >= l0 && lane < l0 + 8) lv = t;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (lane == 0) {
-        double* stk = scratch + kPwMaxLeaves;
-        int sp = 0;
-        for (int o = 0; o < pl.nops; ++o) {
-            const int op = pl.ops[o];
-            if (op >= 0) {
-                stk[sp++] = scratch[op];
-            } else {
-                const double b = stk[--sp];
-                const double x = stk[--sp];
-                stk[sp++] = x + b;
-            }
-        }
-        res = 0.0 + stk[0];
+    for (int rd = 0; rd < pl.nrounds; ++rd) {
+        const int p = lane < kPwMaxLeaves ? pl.partner[rd][lane] : -1;
+        const double v = __shfl(lv, p >= 0 ? p : lane);
+        if (p >= 0) lv = lv + v;
     }
-    return __shfl(res, 0);
+    return 0.0 + __shfl(lv, 0);
 }
 
 template <int DT>
@@ -202,21 +206,6 @@ __device__ __forceinline__ void chunk_add(const uint32_t (&u)[4], double* acc) {
     }
 }
 
-template <int DT>
-__device__ __forceinline__ void chunk_add_masked(const uint32_t (&u)[4], double* acc, bool live) {
-    if constexpr (DT == kF32) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] += live ? (double)__uint_as_float(u[e]) : 0.0;
-    } else if constexpr (DT == kF64) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-            acc[e] += live ? __longlong_as_double((long long)(((uint64_t)u[2 * e + 1] << 32) | u[2 * e])) : 0.0;
-    } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += live ? bf16_to_f64((u[e >> 1] >> (16 * (e & 1))) & 0xffffu) : 0.0;
-    }
-}
-
 // scipy.stats.entropy of the consensus row whose member sums sit in this
 // wave's registers (lane l: chunks l, l+64, ... of CPC classes each), via the
 // per-wave LDS row: mean = acc / M, row sum, entr, row sum (amg_test.py:441-443).
@@ -299,23 +288,23 @@ __device__ inline double wave_item_entropy_vec(const void* p, int64_t off, int M
 }
 
 // One batch of UNR member rows x KCH 16-B chunks per lane of one item (raw
-// words, no conversion until the adds).  Members past M re-load member M-1
-// (in bounds) and are added as +0.0 (bit-exact no-op, see committee_mean_multi).
+// words, no conversion until the adds).  UNR divides M (the host picks UNR = 1
+// otherwise), so every batch is full: plain in-order adds, no masking.
 template <int DT, int KCH, int UNR>
 struct WideBatch {
     uint32_t v[UNR][KCH][4];
 
-    __device__ __forceinline__ void issue(const char* item, int m0, int M, int64_t sMb, int K) {
+    __device__ __forceinline__ void issue(const char* item, int m0, int64_t sMb, int K) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-            const int m = m0 + u < M ? m0 + u : M - 1;
 #pragma unroll
             for (int kk = 0; kk < KCH; ++kk) {
                 const int ch = lane + 64 * kk;
                 const int chs = ch < K ? ch : K - 1;
-                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(item + (int64_t)m * sMb) + chs);
+                const u32x4 x =
+                    __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(item + (int64_t)(m0 + u) * sMb) + chs);
                 v[u][kk][0] = x.x;
                 v[u][kk][1] = x.y;
                 v[u][kk][2] = x.z;
@@ -324,14 +313,12 @@ struct WideBatch {
         }
     }
 
-    __device__ __forceinline__ void add(double* acc, int m0, int M) const {
+    __device__ __forceinline__ void add(double* acc) const {
         constexpr int CPC = ChunkT<DT>::CPC;
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const bool live = m0 + u < M;
+        for (int u = 0; u < UNR; ++u)
 #pragma unroll
-            for (int kk = 0; kk < KCH; ++kk) chunk_add_masked<DT>(v[u][kk], acc + kk * CPC, live);
-        }
+            for (int kk = 0; kk < KCH; ++kk) chunk_add<DT>(v[u][kk], acc + kk * CPC);
     }
 };
 
@@ -344,7 +331,7 @@ struct WideArgs {
     bool pow2;
 };
 
-// LDS per wave: C row + scratch.
-__host__ __device__ constexpr int wide_lds_doubles(int C) { return ((C + kPwMaxLeaves + 8 + 1) / 2) * 2; }
+// LDS per wave: the C-double row.
+__host__ __device__ constexpr int wide_lds_doubles(int C) { return ((C + 1) / 2) * 2; }  // the row (16-B multiple)
 
 }  // namespace ce
