@@ -11,7 +11,8 @@ top-q with one RCCL all-gather before an identical merge on every rank.
 
 One step = the full selection: fused score + per-block top-q over the resident
 shard (stage 1, the streaming kernel), the merge of the blocks' candidates
-(stage 2), and for N > 1 the all-gather + merge.  Inputs are synthetic
+(stage 2), and for N > 1 the all-gather of every rank's q candidate records
+(16 B each) + the merge.  Inputs are synthetic
 Dirichlet(1) member rows (1% un-normalised, like sigmoid CNN members), seed
 1987, generated on the device before timing.
 
@@ -160,14 +161,25 @@ def main():
     log(f"[rank {rank}] pool shard {n_local} x {M} x {C} fp32 ({P.numel() * 4 / 1e9:.1f} GB) "
         f"generated in {time.time() - t0:.1f}s")
     plan = ops.MCPlan(P, q, args.layout, base_idx=lo)
+    # N > 1: stage 2 writes this rank's q candidate records (ce_cand, 16 B each)
+    # straight into the all-gather send buffer; the merge reads the receive
+    # buffer as is -- per step: stage 1, stage 2, one RCCL all-gather, merge.
+    send = torch.empty((q, 2), dtype=torch.int64, device=device)
+    recv = torch.empty((world * q, 2), dtype=torch.int64, device=device)
+
+    def finish():
+        if world == 1:
+            return plan.finish()
+        if q > 64:  # records need q <= 64: exchange packed (entropy, position) pairs instead
+            vals, idx = plan.finish()
+            return ops.topq_merge(*cdist.allgather_topq(vals, idx, q), q)
+        plan.finish_cands(send)
+        cdist.allgather_cands(send, out=recv)
+        return ops.merge_cands(recv, q)
 
     def step():
         plan.partial()
-        vals, idx = plan.finish()
-        if world > 1:
-            av, ai = cdist.allgather_topq(vals, idx, q)
-            vals, idx = ops.topq_merge(av, ai, q)
-        return vals, idx
+        return finish()
 
     for _ in range(args.warmup):
         step()
@@ -181,10 +193,7 @@ def main():
         ev[k][0].record(stream)
         plan.partial()
         ev[k][1].record(stream)
-        vals, idx = plan.finish()
-        if world > 1:
-            av, ai = cdist.allgather_topq(vals, idx, q)
-            vals, idx = ops.topq_merge(av, ai, q)
+        vals, idx = finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

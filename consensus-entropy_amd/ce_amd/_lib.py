@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(_HERE, "libce_amd.so")
 CE_OK, CE_EINVAL, CE_EWORKSPACE, CE_ELAUNCH, CE_EUNSUPPORTED = 0, -1, -2, -3, -4
 CE_F32, CE_F64, CE_BF16 = 0, 1, 2
 CE_MAX_Q = 2048
+CE_CAND_MAX_Q = 64  # ce_select_finish_cands / ce_merge_cands
 
 # name -> (restype, argtypes); the exact export list of include/ce.h
 _vp, _i64, _i32, _sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t
@@ -39,6 +40,8 @@ SIGNATURES = {
     "ce_select_mc": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),
     "ce_select_mc_partial": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _i32, _i64, _vp, _sz, _vp]),
     "ce_select_finish": (_int, [_i64, _i32, _vp, _sz, _vp, _vp, _vp]),
+    "ce_select_finish_cands": (_int, [_i64, _i32, _vp, _sz, _vp, _vp]),
+    "ce_merge_cands": (_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
     "ce_select_mix_workspace_bytes": (_sz, [_i64, _i64, _i32]),
     "ce_select_mix": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _sz,
                              _vp, _vp, _vp]),

@@ -8,6 +8,10 @@ and every rank runs the same deterministic merge.  Exact: the global top-q is a
 subset of the union of the local top-qs, and the merge uses the same total
 order (NaN first, entropy descending, lowest position).
 
+Two exchange formats: (f64 entropy, i64 position) pairs packed into one i64
+tensor (any q), or -- for q <= 64, what bench.py uses -- the engine's 16-byte
+candidate records (ce_cand), written by stage 2 straight into the all-gather
+send buffer and merged from the receive buffer as is (no pack/unpack kernels).
 The local-select and merge steps are injectable so the collective logic can be
 exercised on CPU with the gloo backend (tests/test_dist.py); by default they
 are the HIP operators.
@@ -45,6 +49,42 @@ def allgather_topq(vals, idx, q, group=None):
     recv = torch.empty(world * send.numel(), dtype=send.dtype, device=send.device)
     dist.all_gather_into_tensor(recv, send, group=group)
     return unpack(recv, q, world)
+
+
+def allgather_cands(cands, group=None, out=None):
+    """All-gather every rank's q candidate records (int64 [q, 2] = ce_cand
+    {order key, position}, from MCPlan.finish_cands): returns [world*q, 2],
+    rank-major -- one RCCL collective of 16q bytes per rank and no pack/unpack
+    kernels; ops.merge_cands reads the receive buffer as is."""
+    world = dist.get_world_size(group)
+    if out is None:
+        out = torch.empty((world * cands.shape[0], 2), dtype=cands.dtype, device=cands.device)
+    dist.all_gather_into_tensor(out, cands.contiguous(), group=group)
+    return out
+
+
+def sharded_select_mc_records(P_local, q, *, global_offset, layout="NMC", group=None, local_records=None,
+                              merge_records=None):
+    """sharded_select_mc over the record exchange (q <= 64): stage 1 + stage 2
+    write this rank's q records straight into the all-gather send buffer, and
+    the merge reads the receive buffer.
+
+    local_records  f(P_local, q, base_idx) -> int64 [q, 2] records; default
+                   the HIP stages (ops.MCPlan + finish_cands)
+    merge_records  f(records [world*q, 2], q) -> (vals, idx); default
+                   ops.merge_cands (HIP)
+    """
+    if local_records is None:
+        def local_records(P, qq, base):
+            plan = ops.MCPlan(P, qq, layout, base_idx=base)
+            plan.partial()
+            return plan.finish_cands()
+    if merge_records is None:
+        merge_records = ops.merge_cands
+    rec = local_records(P_local, q, int(global_offset))
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        rec = allgather_cands(rec, group)
+    return merge_records(rec, q)
 
 
 def sharded_select_mc(P_local, q, *, global_offset, layout="NMC", group=None, local_select=None, merge=None):

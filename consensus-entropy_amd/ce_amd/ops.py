@@ -185,9 +185,36 @@ class MCPlan:
              _stream(self.P.device))
         return self.vals, self.idx
 
+    def finish_cands(self, out=None):
+        """Stage 2 writing this pool's q candidate records (ce_cand: order key,
+        position; as an int64 [q, 2] tensor) -- the all-gather send buffer of
+        the multi-GPU merge.  q <= 64."""
+        if out is None:
+            out = torch.empty((self.q, 2), dtype=torch.int64, device=self.P.device)
+        call("ce_select_finish_cands", self.N, self.q, _p(self.ws), self.ws_bytes, _p(out), _stream(self.P.device))
+        return out
+
     def __call__(self):
         self.partial()
         return self.finish()
+
+
+def merge_cands(cands, q):
+    """Merge nlists lists of q candidate records (int64 [nlists*q, 2] or
+    [nlists, q, 2], each list best-first -- e.g. the all-gather receive buffer)
+    into the final (vals [q], idx [q])."""
+    _on_gpu(cands, "cands")
+    q = _check_q(q)
+    if q > _lib.CE_CAND_MAX_Q:
+        raise ValueError(f"candidate records need q <= {_lib.CE_CAND_MAX_Q}")
+    if cands.dtype != torch.int64 or cands.shape[-1] != 2 or not cands.is_contiguous():
+        raise ValueError("cands must be a contiguous int64 [..., 2] tensor of records")
+    n = cands.numel() // 2
+    if n % q:
+        raise ValueError("cands must hold nlists * q records")
+    ov, oi = _outs(q, cands.device)
+    call("ce_merge_cands", _p(cands), n // q, q, _p(ov), _p(oi), _stream(cands.device))
+    return ov, oi
 
 
 def select_mix(P, hc, q, layout="MNC"):

@@ -512,20 +512,55 @@ __global__ __launch_bounds__(kHeadsBS) void k_finish_heads(ListSrc<FROM_VALS> sr
     write_list<2048, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
 }
 
-// Stage 2 for q <= 64: 16 waves stream the candidates (64 consecutive per wave
-// per step, PF steps in flight) through register top-q lists -- after the
-// first chunk almost nothing beats a wave's threshold -- and the 16 lists are
-// tree-merged.  No LDS buffer, no block barrier until the final merge.
+// Stage 2 for q <= 64.  The lists are best-first, so a list's head is its
+// best entry.  Phase 1: each of the 16 waves sorts the heads of its share of
+// the lists (one per lane) in registers; its q-th best head T_w is an exact
+// lower bound (q distinct lists have an entry >= T_w), and so is T = the best
+// T_w.  Phase 2: the waves stream all candidates (64 consecutive per wave per
+// step, PF steps in flight) through register top-q lists floored at T -- only
+// candidates >= T (~q of them) are ever inserted -- and the lists are
+// tree-merged.  Output: final (val, idx), or candidate records (wc) for an
+// exchange between ranks.
 template <bool FROM_VALS>
 __global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int nl, int q,
-                                                    double* __restrict__ oval, int64_t* __restrict__ oidx) {
+                                                    double* __restrict__ oval, int64_t* __restrict__ oidx,
+                                                    Cand* __restrict__ ocand) {
     __shared__ WaveListsT<16> sm;
+    __shared__ uint64_t bk[16];
+    __shared__ int64_t bi[16];
     constexpr int PF = 4;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
     const int64_t L = (int64_t)nl * q;
+    // phase 1: the head bound (only worth a sort when there are many lists)
+    uint64_t fk = 0;
+    int64_t fi = INT64_MAX;
+    if (nl > 64) {
+        RegTopQ hq;
+        hq.init(q);
+        for (int g0 = w * 64; g0 < nl; g0 += 16 * 64) {
+            const int g = g0 + lane;
+            uint64_t k = 0;
+            int64_t id = -1;
+            src.get(seg0 + (int64_t)(g < nl ? g : nl - 1) * q, k, id);
+            hq.offer(k, id, g < nl && id >= 0);
+        }
+        const uint64_t qk = readlane64(hq.k, q - 1);
+        const int64_t qi = (int64_t)readlane64((uint64_t)hq.i, q - 1);
+        if (lane == 0) {
+            bk[w] = qk;
+            bi[w] = qi;
+        }
+        __syncthreads();
+        for (int v = 0; v < 16; ++v)
+            if (bi[v] != INT64_MAX && better(bk[v], bi[v], fk, fi)) {
+                fk = bk[v];
+                fi = bi[v];
+            }
+        if (fi != INT64_MAX) fi += 1;  // admit candidates >= T: strictly better than (T.key, T.idx + 1)
+    }
     RegTopQ tq;
-    tq.init(q);
+    tq.init(q, fk, fi);
     for (int64_t c0 = (int64_t)w * 64; c0 < L; c0 += (int64_t)16 * 64 * PF) {
         uint64_t k[PF];
         int64_t id[PF];
@@ -538,7 +573,11 @@ __global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int 
 #pragma unroll
         for (int u = 0; u < PF; ++u) tq.offer(k[u], id[u], id[u] >= 0);
     }
-    block_merge_write<16>(tq, sm, q, nullptr, 0, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    if (ocand)
+        block_merge_write<16>(tq, sm, q, ocand + slot, 0);
+    else
+        block_merge_write<16>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot);
 }
 
 // ---------------------------------------------------------------------------
@@ -701,12 +740,14 @@ static bool merge_reg_enabled() {
     return on;
 }
 
+// ocand != nullptr: write candidate records (q <= kStreamMaxQ only) instead of (val, idx).
 template <bool FROM_VALS>
 static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, double* oval, int64_t* oidx,
-                          hipStream_t st) {
+                          hipStream_t st, Cand* ocand = nullptr) {
     const int64_t L = (int64_t)nl * q;
-    if (q <= kStreamMaxQ && merge_reg_enabled()) {
-        hipLaunchKernelGGL((k_merge_reg<FROM_VALS>), dim3(segments), dim3(1024), 0, st, src, nl, q, oval, oidx);
+    if (q <= kStreamMaxQ && (merge_reg_enabled() || ocand)) {
+        hipLaunchKernelGGL((k_merge_reg<FROM_VALS>), dim3(segments), dim3(1024), 0, st, src, nl, q, oval, oidx,
+                           ocand);
         return;
     }
     if (q <= kHeadsMaxQ && L > 256) {
@@ -1189,6 +1230,34 @@ extern "C" int ce_select_finish(int64_t N, int32_t q, void* ws, size_t ws_bytes,
     if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
     finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, (hipStream_t)stream);
     return check_launch("ce_select_finish");
+}
+
+// ---- exchange records (multi-GPU) -------------------------------------------
+static_assert(sizeof(ce_cand) == sizeof(Cand) && alignof(ce_cand) <= alignof(Cand), "ce_cand must mirror Cand");
+
+extern "C" int ce_select_finish_cands(int64_t N, int32_t q, void* ws, size_t ws_bytes, ce_cand* out,
+                                      ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "candidate records need q <= %d (got %d)", kStreamMaxQ, q);
+    if (N < 0 || !out) return fail(CE_EINVAL, "bad finish arguments");
+    if ((uintptr_t)out % 16) return fail(CE_EINVAL, "ce_cand output must be 16-byte aligned");
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    ListSrc<false> ls{carve(ws, G, q).c, nullptr, nullptr};
+    launch_finish(ls, 1, G, q, nullptr, nullptr, (hipStream_t)stream, reinterpret_cast<Cand*>(out));
+    return check_launch("ce_select_finish_cands");
+}
+
+extern "C" int ce_merge_cands(const ce_cand* c, int32_t nlists, int32_t q, double* val_out, int64_t* idx_out,
+                              ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (nlists < 1 || !c || !val_out || !idx_out) return fail(CE_EINVAL, "bad merge arguments");
+    if ((uintptr_t)c % 16) return fail(CE_EINVAL, "ce_cand input must be 16-byte aligned");
+    ListSrc<false> ls{reinterpret_cast<const Cand*>(c), nullptr, nullptr};
+    launch_finish(ls, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
+    return check_launch("ce_merge_cands");
 }
 
 // ---- fused mix ---------------------------------------------------------------

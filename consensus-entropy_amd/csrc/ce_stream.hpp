@@ -90,22 +90,30 @@ __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t b
 struct RegTopQ {
     uint64_t k;   // this lane's slot
     int64_t i;
-    uint64_t tk;  // threshold = slot q-1 (wave-uniform)
+    uint64_t tk;  // threshold = the better of slot q-1 and the floor (wave-uniform)
     int64_t ti;
+    uint64_t fk;  // floor: a known exact lower bound (only candidates beating it can be selected)
+    int64_t fi;
     int q;
 
-    __device__ __forceinline__ void init(int q_) {
+    __device__ __forceinline__ void init(int q_, uint64_t fk_ = 0, int64_t fi_ = INT64_MAX) {
         k = 0;
         i = INT64_MAX;
-        tk = 0;
-        ti = INT64_MAX;
+        tk = fk = fk_;
+        ti = fi = fi_;
         q = q_;
     }
 
     __device__ __forceinline__ void refresh() {
-        tk = readlane64(k, q - 1);
-        ti = (int64_t)readlane64((uint64_t)i, q - 1);
+        const uint64_t sk = readlane64(k, q - 1);
+        const int64_t si = (int64_t)readlane64((uint64_t)i, q - 1);
+        const bool s_better = better(sk, si, fk, fi);
+        tk = s_better ? sk : fk;
+        ti = s_better ? si : fi;
     }
+
+    // the list holds no candidate (wave-uniform)
+    __device__ __forceinline__ bool empty() const { return readlane64((uint64_t)i, 0) == (uint64_t)INT64_MAX; }
 
     // insert one wave-uniform candidate that beats the threshold
     __device__ __forceinline__ void insert(uint64_t ck, int64_t ci) {
@@ -143,7 +151,12 @@ struct RegTopQ {
             uint64_t bk = pass ? ck : 0ull;
             int64_t bi = pass ? ci : INT64_MAX;
             wave_sort64(bk, bi);
-            wave_merge64(k, i, bk, bi);
+            if (empty()) {
+                k = bk;
+                i = bi;
+            } else {
+                wave_merge64(k, i, bk, bi);
+            }
             refresh();
         }
     }
@@ -267,7 +280,18 @@ __device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L
             L.idx[w][lane] = i;
         }
         __syncthreads();
-        if ((w & (2 * s - 1)) == 0) wave_merge64(k, i, L.key[w + s][lane], L.idx[w + s][lane]);
+        if ((w & (2 * s - 1)) == 0) {
+            const uint64_t bk = L.key[w + s][lane];
+            const int64_t bi = L.idx[w + s][lane];
+            if (readlane64((uint64_t)bi, 0) != (uint64_t)INT64_MAX) {  // partner list not empty
+                if (readlane64((uint64_t)i, 0) == (uint64_t)INT64_MAX) {
+                    k = bk;  // own list empty: take the partner's as is
+                    i = bi;
+                } else {
+                    wave_merge64(k, i, bk, bi);
+                }
+            }
+        }
     }
     if (w == 0 && lane < q) {
         const bool ok = i != INT64_MAX;

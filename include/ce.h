@@ -123,6 +123,30 @@ int ce_select_finish(int64_t N, int32_t q, void *ws, size_t ws_bytes, double *va
                      int64_t *idx_out, ce_stream_t stream);
 
 /*
+ * Exchange records for the multi-GPU merge (BASELINE.json north_star: "each GPU
+ * computes its local top-q, an RCCL allgather over xGMI collects the
+ * candidates, and a merge produces the final q").  A ce_cand is 16 bytes of
+ * plain data: `key` is an order key monotone in the selection order (NaN first,
+ * entropy descending; compare as unsigned), `idx` the global position, -1 for
+ * an empty slot.  A list is q records, best first.
+ *   ce_select_finish_cands  stage 2 of ce_select_mc_partial, writing the rank's
+ *                           q records to `out` (the all-gather send buffer)
+ *   ce_merge_cands          merge nlists such lists (the all-gather receive
+ *                           buffer, rank-major) into the final top-q
+ * Both need q <= 64 (CE_EUNSUPPORTED otherwise: use ce_select_finish +
+ * ce_topq_merge) and 16-byte aligned record buffers.
+ */
+typedef struct {
+    uint64_t key;
+    int64_t idx;
+} ce_cand;
+
+int ce_select_finish_cands(int64_t N, int32_t q, void *ws, size_t ws_bytes, ce_cand *out,
+                           ce_stream_t stream);
+int ce_merge_cands(const ce_cand *c, int32_t nlists, int32_t q, double *val_out, int64_t *idx_out,
+                   ce_stream_t stream);
+
+/*
  * Fused mix selection -- replaces amg_test.py:473-480: the ROW stack
  * [mc consensus (N rows); hc table (N_h rows)], entropy, top-q over the union.
  * Positions in [0, N) are committee items, [N, N + N_h) hc rows.

@@ -36,6 +36,88 @@ def _oracle_merge(vals, idx, q):
     return torch.from_numpy(v), torch.from_numpy(i)
 
 
+def _order_key(h):
+    """The engine's order key (ce_device.hpp order_key) restated in numpy for
+    the record-exchange test: NaN -> max, -0.0 -> +0.0, monotone in the order."""
+    h = np.asarray(h, np.float64) + 0.0
+    b = h.view(np.uint64)
+    k = np.where(b >> np.uint64(63), ~b, b | np.uint64(1 << 63))
+    return np.where(np.isnan(h), np.uint64(0xFFFFFFFFFFFFFFFF), k)
+
+
+def _key_to_val(k):
+    k = np.asarray(k, np.uint64)
+    b = np.where(k >> np.uint64(63), k & np.uint64(0x7FFFFFFFFFFFFFFF), ~k)
+    v = b.view(np.float64).copy()
+    v[k == np.uint64(0xFFFFFFFFFFFFFFFF)] = np.nan
+    return v
+
+
+def _oracle_local_records(P, q, base):
+    v, i = _oracle_local(P, q, base)
+    rec = np.zeros((q, 2), np.int64)
+    ok = i.numpy() >= 0
+    rec[:, 0] = np.where(ok, _order_key(v.numpy()), 0).view(np.int64)
+    rec[:, 1] = i.numpy()
+    return torch.from_numpy(rec)
+
+
+def _oracle_merge_records(rec, q):
+    r = rec.numpy()
+    vals = _key_to_val(r[:, 0].view(np.uint64))
+    return _oracle_merge(torch.from_numpy(vals), torch.from_numpy(r[:, 1].copy()), q)
+
+
+def _worker_records(rank, world, port, N, q, seed, out):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "consensus-entropy_amd"))
+    from ce_amd import dist as cdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P = _pool(N, seed)
+    lo, hi = cdist.shard_range(N, rank, world)
+    v, i = cdist.sharded_select_mc_records(torch.from_numpy(P[lo:hi]), q, global_offset=lo,
+                                           local_records=_oracle_local_records,
+                                           merge_records=_oracle_merge_records)
+    out[rank] = (v.numpy().tolist(), i.numpy().tolist())
+    dist.destroy_process_group()
+
+
+def _pool(N, seed):
+    rng = np.random.default_rng(seed)
+    e = -np.log(rng.random((N, 8, 4)))
+    P = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+    P[::50] = np.floor(P[::50] * 4) / 4  # ties across shard boundaries
+    return P
+
+
+@pytest.mark.parametrize("world,N,q", [(2, 5000, 10), (2, 7, 10), (3, 4001, 25)])
+def test_sharded_records_equal_global(world, N, q):
+    """The record exchange (ce_cand all-gather, rank-major receive buffer)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_records, args=(world, _free_port(), N, q, 7, out), nprocs=world, join=True)
+    vg, ig = O.oracle_select_mc(_pool(N, 7), q, layout="NMC")
+    for r in range(world):
+        v, i = out[r]
+        assert list(i)[:len(ig)] == ig.tolist()
+        assert all(x == -1 for x in list(i)[len(ig):])
+
+
+def test_order_key_roundtrip():
+    h = np.array([np.nan, 1.5, -0.0, 0.0, -np.inf, np.inf, 1e-300, -2.0])
+    k = _order_key(h)
+    back = _key_to_val(k)
+    assert np.array_equal(np.isnan(back), np.isnan(h))
+    assert np.array_equal(back[~np.isnan(h)], (h + 0.0)[~np.isnan(h)])
+    fin = ~np.isnan(h)
+    order = np.argsort(k[fin])
+    assert np.all(np.diff((h[fin] + 0.0)[order]) >= 0)
+
+
 def _worker(rank, world, port, N, q, seed, out):
     import sys
 

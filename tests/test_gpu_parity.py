@@ -340,3 +340,30 @@ def test_small_pool_single_launch(ce, N):
     for q in (1, 10, 64):
         _, idx = ce.ops.select_mc(dev(np.transpose(P, (1, 0, 2))), q, "MNC")
         assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, q, "NMC")[1]), q
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_record_exchange(ce, world):
+    """The multi-GPU exchange on one device: each 'rank' scores its shard
+    (stage 1 + stage 2 into ce_cand records), the records are concatenated
+    rank-major as the all-gather leaves them, and ce_merge_cands gives the
+    global top-q."""
+    from ce_amd import dist as cdist
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(world)
+    N, q = 300_001, 10
+    P = synth(rng, N, 16, 4, quant=32)
+    Pd = dev(P)
+    recs = []
+    for r in range(world):
+        lo, hi = cdist.shard_range(N, r, world)
+        plan = ce.ops.MCPlan(Pd[lo:hi], q, "NMC", base_idx=lo)
+        plan.partial()
+        recs.append(plan.finish_cands())
+    vals, idx = ce.ops.merge_cands(torch.cat(recs), q)
+    vo, io = O.oracle_select_mc(P, q, "NMC")
+    assert np.array_equal(idx_np(idx), io)
+    assert_ent_close(vals.cpu().numpy()[: len(io)], vo)
+    with pytest.raises(ValueError):
+        ce.ops.merge_cands(torch.cat(recs), 65)
