@@ -528,10 +528,22 @@ __global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int 
     __shared__ WaveListsT<16> sm;
     __shared__ uint64_t bk[16];
     __shared__ int64_t bi[16];
-    constexpr int PF = 4;
+    constexpr int PF = 10;  // 16 x 64 x 10: 1024 lists of q = 10 in one round of loads
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
     const int64_t L = (int64_t)nl * q;
+    // the first round of candidate loads goes out before the head phase
+    uint64_t k[PF];
+    int64_t id[PF];
+    auto load_round = [&](int64_t c0) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int64_t j = c0 + (int64_t)u * 16 * 64 + lane;
+            src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);  // clamped: no branch around a load
+            if (j >= L) id[u] = -1;
+        }
+    };
+    load_round((int64_t)w * 64);
     // phase 1: the head bound (only worth a sort when there are many lists)
     uint64_t fk = 0;
     int64_t fi = INT64_MAX;
@@ -540,10 +552,10 @@ __global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int 
         hq.init(q);
         for (int g0 = w * 64; g0 < nl; g0 += 16 * 64) {
             const int g = g0 + lane;
-            uint64_t k = 0;
-            int64_t id = -1;
-            src.get(seg0 + (int64_t)(g < nl ? g : nl - 1) * q, k, id);
-            hq.offer(k, id, g < nl && id >= 0);
+            uint64_t hk = 0;
+            int64_t hid = -1;
+            src.get(seg0 + (int64_t)(g < nl ? g : nl - 1) * q, hk, hid);
+            hq.offer(hk, hid, g < nl && hid >= 0);
         }
         const uint64_t qk = readlane64(hq.k, q - 1);
         const int64_t qi = (int64_t)readlane64((uint64_t)hq.i, q - 1);
@@ -562,14 +574,7 @@ __global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int 
     RegTopQ tq;
     tq.init(q, fk, fi);
     for (int64_t c0 = (int64_t)w * 64; c0 < L; c0 += (int64_t)16 * 64 * PF) {
-        uint64_t k[PF];
-        int64_t id[PF];
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-            const int64_t j = c0 + (int64_t)u * 16 * 64 + lane;
-            src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);  // clamped: no branch around a load
-            if (j >= L) id[u] = -1;
-        }
+        if (c0 != (int64_t)w * 64) load_round(c0);
 #pragma unroll
         for (int u = 0; u < PF; ++u) tq.offer(k[u], id[u], id[u] >= 0);
     }
@@ -933,7 +938,14 @@ static void with_batching(int M, F&& f) {
     }
 }
 
-// The same for k_stream_seg: 16-wave blocks (<= 128 VGPRs), so fewer loads per lane.
+// Waves per user block of ce_select_batched: 8 for many users (two 8-wave
+// blocks per CU keep ~512 users resident at once), 16 for a few large ones.
+static int user_waves(int64_t total, int U) {
+    const int64_t avg = total / (U > 0 ? U : 1);
+    return (U >= 256 || avg < 4096) ? 8 : 16;
+}
+
+// The same for k_stream_seg: up to 16-wave blocks (<= 128 VGPRs), so fewer loads per lane.
 template <class Src, class F>
 static void with_seg_batching(F&& f) {
     if constexpr (Src::kC > 4) f(std::integral_constant<int, 4>(), std::integral_constant<int, 1>());
@@ -1326,7 +1338,7 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
         rc = with_committee(a, [&](auto src) {
             using S = decltype(src);
             with_seg_batching<S>([&](auto unr, auto ipl) {
-                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(U), dim3(64 * kSegWaves),
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(U), dim3(64 * user_waves(total_items, U)),
                                    0, st, src, offsets, (int64_t)0, (int64_t)0, q, val_out, idx_out);
             });
         });

@@ -263,9 +263,10 @@ struct StreamArgs {
 // outputs.  A tree over the waves: at level s, waves w = s mod 2s park their
 // list in LDS and waves w = 0 mod 2s merge it in (7 shuffle stages); every
 // LDS slot is written once and read once, one barrier per level.
+// nw = waves taking part (a power of two <= WAVES; default all of them).
 template <int WAVES>
 __device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L, int q, Cand* wc, int nlists,
-                                         double* oval = nullptr, int64_t* oidx = nullptr) {
+                                         double* oval = nullptr, int64_t* oidx = nullptr, int nw = WAVES) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // empty lists for the workspace slots no block of this (occupancy-sized)
     // grid owns: b + gridDim.x, b + 2*gridDim.x, ...
@@ -273,8 +274,7 @@ __device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L
         for (int r = threadIdx.x; r < q; r += blockDim.x) wc[(s - blockIdx.x) * q + r] = Cand{0ull, -1};
     uint64_t k = tq.k;
     int64_t i = tq.i;
-#pragma unroll
-    for (int s = 1; s < WAVES; s <<= 1) {
+    for (int s = 1; s < WAVES && s < nw; s <<= 1) {  // block-uniform bound
         if ((w & (2 * s - 1)) == s) {
             L.key[w][lane] = k;
             L.idx[w][lane] = i;
@@ -384,12 +384,13 @@ template <class Src, int IPL, int UNR, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int64_t n,
                                                             int64_t base_idx, int q, double* __restrict__ oval,
                                                             int64_t* __restrict__ oidx) {
+    // launched with WAVES or fewer waves (a power of two): blockDim.x / 64
     __shared__ WaveListsT<WAVES> sm;
-    const int w = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int64_t s0 = offsets ? offsets[blockIdx.x] : 0, s1 = offsets ? offsets[blockIdx.x + 1] : n;
     const int64_t len = s1 > s0 ? s1 - s0 : 0;
     constexpr int64_t kIt = 64 * IPL;
-    const int64_t per = ((len + kIt - 1) / kIt + WAVES - 1) / WAVES * kIt;
+    const int64_t per = ((len + kIt - 1) / kIt + nw - 1) / nw * kIt;
     int64_t lo = s0 + w * per;
     int64_t hi = lo + per < s1 ? lo + per : s1;
     if (lo > hi) lo = hi;
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_
     tq.init(q);
     stream_direct_range<Src, IPL, UNR>(src, lo, hi, (offsets ? 0 : base_idx) - s0, q, tq);
     const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write<WAVES>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot);
+    block_merge_write<WAVES>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot, nw);
 }
 
 }  // namespace ce
