@@ -1291,10 +1291,19 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     if (!ws || ws_bytes < lists_bytes((int64_t)G1 + G2, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, (int64_t)G1 + G2, q);
-    Seg s1{nullptr, N, G1, 0};
-    rc = committee_partial(a, s1, G1, q, w, nullptr, nullptr, false, st);
-    if (rc) return dispatch_err(rc, a);
+    // both segments on the streaming engine when it applies (q <= 64): the hc
+    // table is a committee of M = 1 member ([N_h, 1, C] f64, row stride ld_hc)
+    if (!launch_stream(a, G1, q, 0, w, st)) {
+        Seg s1{nullptr, N, G1, 0};
+        rc = committee_partial(a, s1, G1, q, w, nullptr, nullptr, false, st);
+        if (rc) return dispatch_err(rc, a);
+    }
     WsLists w2{w.c + (size_t)G1 * q};
+    const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
+    if (launch_stream(t, G2, q, N, w2, st)) {
+        finish_lists(w, 1, G1 + G2, q, val_out, idx_out, st);
+        return check_launch("ce_select_mix");
+    }
     Seg s2{nullptr, N_h, G2, N};
     switch (C) {
 #define CE_T(CC) case CC: launch_partial(TableSrc<CC>{hc, ld_hc}, s2, G2, q, w2, nullptr, nullptr, false, st); break;

@@ -48,6 +48,15 @@ profile)
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/write_$LAYOUT" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --layout "$LAYOUT" > "$OUT/prof_write_$LAYOUT.log" 2>&1
   step $? "write $LAYOUT"
   ;;
-*) echo "PHASE must be check or profile" >&2; exit 2 ;;
+configs)  # kernel-trace stats of every secondary config + FETCH/WRITE passes of the wide one
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof/configs" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" > "$OUT/prof_configs.log" 2>&1
+  step $? "trace configs"
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/fetch_wide" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" --only 4 > "$OUT/prof_fetch_wide.log" 2>&1
+  step $? "fetch wide"
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/write_wide" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" --only 4 > "$OUT/prof_write_wide.log" 2>&1
+  step $? "write wide"
+  ;;
+*) echo "PHASE must be check, ab, profile or configs" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"

@@ -62,4 +62,32 @@ for layout in ("NMC", "MNC"):
                         "fetch_KiB": pmc[k].get("FETCH_SIZE_KiB_mean"), "write_KiB": pmc[k].get("WRITE_SIZE_KiB_mean"),
                         "source": f"profiles/{tag}_{layout}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"}
     print(layout, json.dumps(pmc, indent=1)[:1500])
+# secondary configs (tools/bench_configs.py): stats of every kernel, PMC of the wide stream
+cdir = os.path.join(prof, "configs")
+if os.path.isdir(cdir):
+    rows = list(csv.reader(open(os.path.join(cdir, "run_kernel_stats.csv"))))
+    head, body = rows[0], rows[1:]
+    body.sort(key=lambda r: (not r[0].startswith("void ce::"), -float(r[2])))
+    with open(os.path.join(out_dir, f"{tag}_configs_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(head)
+        w.writerows(body)
+pmc = {}
+for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    path = os.path.join(prof, f"{counter.split('_')[0].lower()}_wide", "run_counter_collection.csv")
+    if not os.path.exists(path):
+        continue
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if r["Kernel_Name"].startswith("void ce::"):
+            vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    for k, v in vals.items():
+        pmc.setdefault(k, {})[counter + "_KiB_mean"] = statistics.mean(v)
+        pmc[k]["dispatches"] = len(v)
+for k in pmc:
+    pmc[k]["hbm_bytes_per_launch"] = (pmc[k].get("FETCH_SIZE_KiB_mean", 0.0) * 1024 * 2
+                                      + pmc[k].get("WRITE_SIZE_KiB_mean", 0.0) * 1024)
+if pmc:
+    json.dump(pmc, open(os.path.join(out_dir, f"{tag}_wide_pmc.json"), "w"), indent=1)
+    print("wide", json.dumps(pmc, indent=1)[:800])
 json.dump(traffic, open(traffic_path, "w"), indent=1)
