@@ -64,11 +64,86 @@ def report(name, items, bytes_, t, extra=None):
     print(json.dumps(d), flush=True)
 
 
+def cpu_reference(only, reps=5):
+    """The reference's own expressions (amg_test.py:441-445 mc, :109-117 +
+    :451-452 hc, :473-480 mix, the per-user loop for configs[2]) timed on the
+    host, numpy single-threaded, same shapes -- median of `reps` after a
+    warm-up.  Restated here (not imported from oracle/, which only tests and
+    bench.py's cpu_baseline may use)."""
+    import statistics
+
+    import numpy as np
+    import pandas as pd
+    from scipy.stats import entropy
+
+    rng = np.random.default_rng(1987)
+
+    def dir_(shape, dt=np.float64):
+        e = -np.log(rng.random(shape))
+        return (e / e.sum(-1, keepdims=True)).astype(dt)
+
+    def med(fn, reps=reps):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    def mc(pred_prob, q=10):
+        consensus_prob = np.mean(np.array(pred_prob), axis=0)
+        ent = entropy(consensus_prob, axis=1)
+        return np.argsort(ent)[::-1][:q]
+
+    out = {}
+    if 0 in only:
+        members = [dir_((1608, 4)), dir_((1608, 4)), dir_((1608, 4), np.float32), dir_((1608, 4), np.float32)]
+        out["configs[0] mc 4x1608x4"] = med(lambda: mc(members))
+    if 1 in only:
+        votes = rng.integers(0, 4, (1608, 665))
+        votes[rng.random((1608, 665)) >= 0.03] = -1
+        votes[:, 0] = 1
+
+        def table():  # amg_test.py:109-117 (per-song Counter + np.round(c/n, 3)) on the vote matrix
+            rows = []
+            for r in votes:
+                v = r[r >= 0]
+                n = len(v)
+                rows.append([np.round(np.count_nonzero(v == c) / n, 3) for c in range(4)])
+            return pd.DataFrame(rows, columns=["Q1", "Q2", "Q3", "Q4"])
+
+        hc = table()
+        out["configs[1] hc table 1608x665 (3%)"] = med(table)
+        out["configs[1] hc select 1608x4"] = med(lambda: np.argsort(entropy(hc, axis=1))[::-1][:10])
+        members = [pd.DataFrame(dir_((1608, 4)), columns=hc.columns) for _ in range(4)]
+
+        def mix():
+            consensus_prob = pd.DataFrame(np.mean(np.array(members), axis=0), columns=hc.columns)
+            this = pd.concat([consensus_prob, hc])
+            return np.argsort(entropy(this, axis=1))[::-1][:10]
+
+        out["configs[1] mix [4x1608x4 ; 1608x4]"] = med(mix)
+    if 2 in only:
+        users = [[dir_((1608, 4), np.float32) for _ in range(4)] for _ in range(500)]
+        out["configs[2] batched 500 users (per-user loop)"] = med(lambda: [mc(u) for u in users], reps=3)
+    if 4 in only:
+        n = 2000
+        members = [dir_((n, 1000), np.float32) for _ in range(32)]
+        t = med(lambda: mc(members), reps=3)
+        out["configs[4] wide 32x1000 (per item)"] = t / n
+    for k, v in out.items():
+        print(json.dumps({"cpu_reference": k, "s": v, "threads": 1}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="0,1,2,4")
+    ap.add_argument("--cpu", action="store_true", help="also time the reference expressions on the host")
     args = ap.parse_args()
     only = {int(x) for x in args.only.split(",")}
+    if args.cpu:
+        cpu_reference(only)
     g = torch.Generator(device="cuda").manual_seed(1987)
     q = 10
     if 0 in only:  # configs[0]: 4-member committee x 1608 x 4, mixed f32/f64 -> f64 stack
