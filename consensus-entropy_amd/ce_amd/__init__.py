@@ -6,10 +6,11 @@ entropy (hc), their row-stacked union (mix) and the random baseline (rand),
 computed by hand-written gfx950 HIP kernels behind the C-ABI of include/ce.h.
 """
 from ._lib import CE_MAX_Q, CEError, load  # noqa: F401
-from .select import MODES, ConsensusEntropySelector, select_queries, stack_committee  # noqa: F401
+from .select import (MODES, ConsensusEntropySelector, committee_from_frames, select_queries,  # noqa: F401
+                     song_groups, stack_committee)
 
-__all__ = ["select_queries", "ConsensusEntropySelector", "stack_committee", "MODES", "CE_MAX_Q", "CEError",
-           "load", "ops", "dist"]
+__all__ = ["select_queries", "ConsensusEntropySelector", "stack_committee", "committee_from_frames", "song_groups",
+           "MODES", "CE_MAX_Q", "CEError", "load", "ops", "dist"]
 
 
 def __getattr__(name):  # lazy submodules (ops/dist need torch)

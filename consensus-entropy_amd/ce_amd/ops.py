@@ -109,6 +109,36 @@ def va_table(va):
     return freq, ent
 
 
+def segment_mean(frames, offsets, perm=None, out=None):
+    """amg_test.py:437 groupby(['s_id']).mean() of one member on the device
+    (pandas 1.1.5 group_mean: f64 sequential sums in row order, NaN skipped,
+    float32 input -> float32-rounded result).  frames [F, C] f32/f64; song n
+    owns rows perm[offsets[n]:offsets[n+1]] (or offsets[n]:offsets[n+1]).
+    out: optional [N, C] f32/f64 view with unit column stride (e.g. member m of
+    a committee stack); default a new tensor of the frames' dtype."""
+    _on_gpu(frames, "frames")
+    _on_gpu(offsets, "offsets")
+    if frames.dim() != 2 or frames.dtype not in (torch.float32, torch.float64):
+        raise ValueError("frames must be a 2-D float32/float64 tensor [F, C]")
+    if frames.stride(1) != 1:
+        frames = frames.contiguous()
+    offsets = offsets.to(torch.int64).contiguous()
+    F, C = frames.shape
+    N = offsets.numel() - 1
+    if N < 0:
+        raise ValueError("offsets must hold N + 1 entries")
+    if perm is not None:
+        _on_gpu(perm, "perm")
+        perm = perm.to(torch.int64).contiguous()
+    if out is None:
+        out = torch.empty((N, C), dtype=frames.dtype, device=frames.device)
+    if out.dim() != 2 or tuple(out.shape) != (N, C) or out.stride(1) != 1 or out.dtype not in _DT:
+        raise ValueError(f"out must be an [N={N}, C={C}] float32/float64 view with unit column stride")
+    call("ce_segment_mean", _p(frames), _DT[frames.dtype], F, C, frames.stride(0), _p(perm), _p(offsets), N,
+         _p(out), _DT[out.dtype], out.stride(0), _stream(frames.device))
+    return out
+
+
 def _check_q(q):
     q = int(q)
     if q < 1 or q > _lib.CE_MAX_Q:

@@ -68,6 +68,53 @@ def stack_committee(committee, device=None, layout="MNC"):
     return torch.from_numpy(np.stack(arrs).astype(dt, copy=False)).to(dev), "MNC"
 
 
+def song_groups(s_id):
+    """Host geometry of groupby(['s_id']) (sort=True): the sorted unique song
+    ids, CSR offsets of each song's frames, and the stable permutation that
+    groups the frames (None when they already are, in sorted order)."""
+    ids = np.asarray(getattr(s_id, "values", s_id))
+    uniq, labels = np.unique(ids, return_inverse=True)
+    labels = labels.reshape(-1)
+    offsets = np.concatenate([[0], np.cumsum(np.bincount(labels, minlength=len(uniq)))]).astype(np.int64)
+    perm = None if np.all(labels[1:] >= labels[:-1]) else np.argsort(labels, kind="stable").astype(np.int64)
+    return uniq, offsets, perm
+
+
+def committee_from_frames(members, s_id, device=None):
+    """The committee stack np.array(pred_prob) of amg_test.py:426-441, built on
+    the device.  `members` in mod_list order; each is either a frame-level
+    predict_proba array [F, C] (rows in X_train order, grouped by `s_id` with
+    the segment-mean kernel, :437) or an already song-level [N, C] frame/array
+    (the CNN member, :432-433, taken positionally as np.array does).  Returns
+    (stack [M, N, C] on the device, the sorted song ids of the groupby rows).
+    The stack is float64 unless every member is float32 (np.array's rule)."""
+    dev = _device(device)
+    uniq, offsets, perm = song_groups(s_id)
+    N = len(uniq)
+    F = len(np.asarray(getattr(s_id, "values", s_id)))
+    arrs = [np.asarray(getattr(m, "values", m)) for m in members]
+    if not arrs:
+        raise ValueError("committee has no members")
+    C = arrs[0].shape[1]
+    dts = {a.dtype for a in arrs}
+    dt = torch.float32 if dts == {np.dtype(np.float32)} else torch.float64
+    stack = torch.empty((len(arrs), N, C), dtype=dt, device=dev)
+    offs_d = torch.from_numpy(offsets).to(dev)
+    perm_d = torch.from_numpy(perm).to(dev) if perm is not None else None
+    for m, a in enumerate(arrs):
+        if a.ndim != 2 or a.shape[1] != C:
+            raise ValueError(f"member {m} has shape {a.shape}, expected [*, {C}]")
+        if a.shape[0] == F and (F != N or perm is not None):  # frame-level: groupby mean on the device
+            fr = torch.from_numpy(np.ascontiguousarray(a, dtype=a.dtype if a.dtype in (np.float32, np.float64)
+                                                       else np.float64)).to(dev)
+            ops.segment_mean(fr, offs_d, perm_d, out=stack[m])
+        elif a.shape[0] == N:  # song-level member
+            stack[m] = torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+        else:
+            raise ValueError(f"member {m} has {a.shape[0]} rows: neither {F} frames nor {N} songs")
+    return stack, uniq
+
+
 def _hc_tensor(hc, votes, C, dev):
     if hc is not None:
         arr = np.asarray(getattr(hc, "values", hc), dtype=np.float64) if not isinstance(hc, torch.Tensor) else hc

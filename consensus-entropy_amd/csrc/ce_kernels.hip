@@ -9,6 +9,7 @@
 //                    final top-q; one block per segment (user / pool).
 //   k_entropy        per-item entropy to HBM (ce_committee_entropy).
 //   k_vote / k_va    hc frequency table + entropy from votes (amg_test.py:88-117).
+//   k_segment_mean   frame -> song mean of one member (groupby mean, amg_test.py:437).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -662,6 +663,49 @@ __global__ __launch_bounds__(kBS) void k_va(const double* __restrict__ va, int64
     }
 }
 
+// ---------------------------------------------------------------------------
+// Frame -> song segment mean: pd.DataFrame(y_probs, index=X_train.index)
+// .groupby(['s_id']).mean() (amg_test.py:437, :469) as pandas 1.1.5's
+// group_mean computes it (the reference pins pandas==1.1.5): values upcast to
+// f64, per (song, class) a sequential sum over the song's frames in row order
+// skipping NaN, divided by the non-NaN count (0 -> NaN); a float32 column is
+// cast back to float32 at the end (the result dtype follows the input).
+// One thread per (song, class); frames of song n are rows perm[off[n]..off[n+1])
+// (perm == nullptr: rows off[n]..off[n+1] themselves, already grouped).
+// ---------------------------------------------------------------------------
+template <int DT, int ODT>
+__global__ __launch_bounds__(kBS) void k_segment_mean(const void* __restrict__ frames, int64_t ld, int C,
+                                                      const int64_t* __restrict__ perm,
+                                                      const int64_t* __restrict__ offsets, int64_t N,
+                                                      void* __restrict__ out, int64_t ldo) {
+    const int64_t total = N * C;
+    for (int64_t t = (int64_t)blockIdx.x * kBS + threadIdx.x; t < total; t += (int64_t)gridDim.x * kBS) {
+        const int64_t n = t / C;
+        const int c = (int)(t - n * C);
+        const int64_t f0 = offsets[n], f1 = offsets[n + 1];
+        double sum = 0.0;
+        int64_t cnt = 0;
+        for (int64_t f = f0; f < f1; ++f) {
+            const int64_t r = perm ? perm[f] : f;
+            double v;
+            if constexpr (DT == kF32)
+                v = (double)static_cast<const float*>(frames)[r * ld + c];
+            else
+                v = static_cast<const double*>(frames)[r * ld + c];
+            if (v == v) {  // not NaN
+                sum += v;
+                ++cnt;
+            }
+        }
+        double m = cnt ? sum / (double)cnt : __longlong_as_double(0x7ff8000000000000ll);
+        if constexpr (DT == kF32) m = (double)(float)m;  // the float32 result column
+        if constexpr (ODT == kF32)
+            static_cast<float*>(out)[n * ldo + c] = (float)m;
+        else
+            static_cast<double*>(out)[n * ldo + c] = m;
+    }
+}
+
 }  // namespace ce
 
 // ===========================================================================
@@ -1128,6 +1172,26 @@ extern "C" int ce_va_entropy(const double* va, int64_t N, int32_t A, double* fre
     const int grid = (int)std::min<int64_t>(cdiv(N, kBS / 64), 8192);
     hipLaunchKernelGGL(k_va, dim3(grid), dim3(kBS), 0, st, va, N, A, freq_or_null, ent);
     return check_launch("ce_va_entropy");
+}
+
+// ---- frame -> song segment mean (amg_test.py:437, :469) ----------------------
+extern "C" int ce_segment_mean(const void* frames, ce_dtype dt, int64_t F, int32_t C, int64_t ld,
+                               const int64_t* perm_or_null, const int64_t* offsets, int64_t N, void* out,
+                               ce_dtype out_dt, int64_t ld_out, ce_stream_t stream) {
+    if (F < 0 || N < 0 || C < 1 || ld < C || ld_out < C) return fail(CE_EINVAL, "bad segment-mean shape");
+    if ((N > 0 && (!offsets || !out)) || (F > 0 && !frames)) return fail(CE_EINVAL, "null pointer");
+    if ((dt != CE_F32 && dt != CE_F64) || (out_dt != CE_F32 && out_dt != CE_F64))
+        return fail(CE_EUNSUPPORTED, "segment mean takes float32/float64 frames and outputs");
+    if (N == 0) return CE_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int grid = (int)std::min<int64_t>(cdiv(N * C, kBS), 8192);
+#define CE_SM(D_, O_)                                                                                        \
+    if (dt == D_ && out_dt == O_)                                                                            \
+        hipLaunchKernelGGL((k_segment_mean<D_, O_>), dim3(grid), dim3(kBS), 0, st, frames, ld, C, perm_or_null, \
+                           offsets, N, out, ld_out);
+    CE_SM(CE_F32, CE_F32) CE_SM(CE_F32, CE_F64) CE_SM(CE_F64, CE_F32) CE_SM(CE_F64, CE_F64)
+#undef CE_SM
+    return check_launch("ce_segment_mean");
 }
 
 // ---- top-q of an entropy vector -------------------------------------------

@@ -88,6 +88,23 @@ int ce_va_entropy(const double *va, int64_t N, int32_t A, double *freq_or_null, 
                   ce_stream_t stream);
 
 /*
+ * Frame -> song segment mean of one committee member -- replaces
+ *   pd.DataFrame(y_probs, index=X_train.index).groupby(['s_id']).mean()
+ * (amg_test.py:437, :469) with pandas 1.1.5 group_mean semantics (the
+ * reference pins pandas==1.1.5): per (song, class) an f64 sequential sum over
+ * the song's frames in row order, NaN skipped, divided by the non-NaN count
+ * (no frame -> NaN); float32 input gives the float32-rounded mean.
+ * frames: [F, C] (dt F32|F64, row stride ld elements).  Song n owns the rows
+ * perm[offsets[n]] .. perm[offsets[n+1]-1] (perm_or_null == NULL: rows
+ * offsets[n] .. offsets[n+1]-1), in their original order; songs are in sorted
+ * s_id order as groupby returns them.  out: [N, C] (out_dt F32|F64, row stride
+ * ld_out) -- e.g. member m's slice of an [M, N, C] committee stack.
+ */
+int ce_segment_mean(const void *frames, ce_dtype dt, int64_t F, int32_t C, int64_t ld,
+                    const int64_t *perm_or_null, const int64_t *offsets, int64_t N, void *out,
+                    ce_dtype out_dt, int64_t ld_out, ce_stream_t stream);
+
+/*
  * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]
  * (amg_test.py:445, :452, :480).  Positions are reported as base_idx + i.
  * val_out: [q] f64, idx_out: [q] int64.

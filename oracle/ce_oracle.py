@@ -64,6 +64,33 @@ def ref_mix(pred_prob, consensus_hc, q):
     return q_ind, ent_mix
 
 
+def ref_group_mean(values, s_id):
+    """amg_test.py:437 ``pd.DataFrame(y_probs, index=X_train.index)
+    .groupby(['s_id']).mean()`` restated with pandas 1.1.5's group_mean (the
+    reference pins pandas==1.1.5; the installed pandas compensates its sums,
+    1.1.5 does not): values upcast to float64 (ensure_float64), per (group,
+    column) a sequential sum in row order skipping NaN (np.add.at applies the
+    additions in index order), divided by the non-NaN count, NaN for none; the
+    result is cast back to float32 for float32 input.  Groups in sorted key
+    order.  Returns (means [N, C], sorted keys)."""
+    v = np.asarray(values)
+    keys, labels = np.unique(np.asarray(s_id), return_inverse=True)
+    labels = labels.reshape(-1)
+    x = v.astype(np.float64)
+    N, C = len(keys), x.shape[1]
+    sumx = np.zeros((N, C))
+    nobs = np.zeros((N, C), np.int64)
+    for j in range(C):
+        ok = ~np.isnan(x[:, j])
+        np.add.at(sumx[:, j], labels[ok], x[ok, j])
+        np.add.at(nobs[:, j], labels[ok], 1)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        out = np.where(nobs > 0, sumx / np.maximum(nobs, 1), np.nan)
+    if v.dtype == np.float32:
+        out = out.astype(np.float32)
+    return out, keys
+
+
 def ref_vote_table(votes, C=4):
     """amg_test.py:109-115 on an int8 vote matrix (-1 = missing): per row,
     Counter over classes, then ``np.round(v / num_anno, 3)``.  Pure-Python loop

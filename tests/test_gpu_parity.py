@@ -367,3 +367,56 @@ def test_record_exchange(ce, world):
     assert_ent_close(vals.cpu().numpy()[: len(io)], vo)
     with pytest.raises(ValueError):
         ce.ops.merge_cands(torch.cat(recs), 65)
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("grouped", [True, False])
+def test_segment_mean_vs_restatement(ce, dt, grouped):
+    """groupby(['s_id']).mean() (amg_test.py:437) on the device, bit-exact vs
+    the pandas-1.1.5 restatement: frames grouped (CSR only) or shuffled (perm),
+    NaN cells, a song whose column is all-NaN, float32 rounding of the result."""
+    from oracle.ce_oracle import ref_group_mean
+
+    rng = np.random.default_rng(11 + grouped)
+    F, C = 50_000, 4
+    s_id = np.sort(rng.integers(0, 1608, F)) if grouped else rng.integers(0, 1608, F)
+    vals = rng.random((F, C)).astype(dt)
+    vals[rng.random((F, C)) < 0.02] = np.nan
+    vals[s_id == s_id[0], 1] = np.nan
+    exp, keys = ref_group_mean(vals, s_id)
+    uniq, offsets, perm = ce.song_groups(s_id)
+    assert np.array_equal(uniq, keys) and (perm is None) == grouped
+    got = ce.ops.segment_mean(dev(vals), dev(offsets), None if perm is None else dev(perm))
+    assert got.dtype == (torch.float32 if dt == np.float32 else torch.float64)
+    assert np.array_equal(got.cpu().numpy(), exp, equal_nan=True)
+    # into an f64 stack slot: the float32 result upcast, as np.array(pred_prob) does
+    slot = torch.empty((2, len(uniq), C), dtype=torch.float64, device="cuda")
+    ce.ops.segment_mean(dev(vals), dev(offsets), None if perm is None else dev(perm), out=slot[1])
+    assert np.array_equal(slot[1].cpu().numpy(), exp.astype(np.float64), equal_nan=True)
+
+
+def test_frames_to_selection(ce):
+    """amg_test.py:426-445 end to end: three frame-level members (f64, f64,
+    f32 -- GNB/SGD/XGB predict_proba over X_train rows) grouped per song on the
+    device plus a song-level member (the CNN), stacked, scored and selected --
+    against the restatement + oracle on the same inputs."""
+    from oracle import ce_oracle as O
+    from oracle.ce_oracle import ref_group_mean
+
+    rng = np.random.default_rng(1987)
+    F, C = 40_000, 4
+    s_id = rng.permutation(np.repeat(np.arange(1608) * 3 + 1, 25))[:F]
+    frame_members = []
+    for dt in (np.float64, np.float64, np.float32):
+        e = -np.log(rng.random((F, C)))
+        frame_members.append((e / e.sum(-1, keepdims=True)).astype(dt))
+    n_songs = len(np.unique(s_id))
+    cnn = rng.random((n_songs, C)).astype(np.float32)  # sigmoid outputs, not normalised
+    members = frame_members + [cnn]
+    stack, uniq = ce.committee_from_frames(members, s_id)
+    assert stack.dtype == torch.float64 and tuple(stack.shape) == (4, n_songs, C)
+    pred_prob = [ref_group_mean(m, s_id)[0] for m in frame_members] + [cnn]
+    P = np.array(pred_prob)  # the reference's stack (mixed -> float64)
+    assert np.array_equal(stack.cpu().numpy(), P)
+    _, idx = ce.ops.select_mc(stack, 10, "MNC")
+    assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, 10, "MNC")[1])

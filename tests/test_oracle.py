@@ -142,3 +142,27 @@ def test_topq_merge_equals_global():
 def test_topq_q_larger_than_n():
     v, i = O.oracle_topq(np.array([0.1, np.nan, 0.3]), 10)
     assert list(i) == [1, 2, 0]
+
+
+def test_group_mean_restatement_vs_pandas():
+    """The pandas-1.1.5 group_mean restatement against the installed pandas on
+    the reference's own expression (amg_test.py:437).  Values are dyadic
+    (multiples of 2**-12, few per group) so every partial sum is exact: the
+    installed pandas' compensated sums and 1.1.5's plain sums then agree bit
+    for bit, and so must the restatement.  NaN cells and unsorted keys too."""
+    import pandas as pd
+
+    from oracle.ce_oracle import ref_group_mean
+
+    rng = np.random.default_rng(437)
+    F, C = 3000, 4
+    s_id = rng.integers(0, 200, F) * 7 + 3
+    vals = rng.integers(0, 4096, (F, C)) / 4096.0
+    vals[rng.random((F, C)) < 0.01] = np.nan
+    for dt in (np.float64, np.float32):
+        v = vals.astype(dt)
+        exp = pd.DataFrame(v, index=pd.Index(s_id, name="s_id")).groupby(["s_id"]).mean()
+        got, keys = ref_group_mean(v, s_id)
+        assert np.array_equal(keys, exp.index.values)
+        assert got.dtype == exp.values.dtype
+        assert np.array_equal(got, exp.values, equal_nan=True)

@@ -138,7 +138,7 @@ def cpu_reference(only, reps=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="0,1,2,4")
+    ap.add_argument("--only", default="0,1,2,4,5")
     ap.add_argument("--cpu", action="store_true", help="also time the reference expressions on the host")
     args = ap.parse_args()
     only = {int(x) for x in args.only.split(",")}
@@ -189,6 +189,25 @@ def main():
         t = timed(lambda: ops.select_mc(chunk, q, "NMC"), nchunks)
         report("configs[4] wide 32x1000 bf16, per 200K-item chunk", Nc, chunk.numel() * 2, t,
                {"est_full_50M_s": t * total / Nc, "wall": time.time() - t0})
+        del chunk
+        torch.cuda.empty_cache()
+    if 5 in only:
+        segment_mean_configs(g, report)
+
+
+def segment_mean_configs(g, report_fn):
+    """the frame -> song groupby mean (amg_test.py:437) per
+    member, frames grouped (CSR) and shuffled (permutation gather)."""
+    for songs, fps in ((1608, 40), (1_000_000, 40)):
+        F, C = songs * fps, 4
+        fr = torch.rand((F, C), device="cuda", generator=g, dtype=torch.float64)
+        offs = torch.arange(0, songs + 1, device="cuda", dtype=torch.int64) * fps
+        t = timed(lambda: ops.segment_mean(fr, offs), 200 if songs < 10_000 else 40)
+        report_fn(f"(f) segment mean {songs} songs x {fps} frames x {C} f64, grouped", F, F * C * 8 + songs * C * 8, t)
+        perm = torch.randperm(F, device="cuda", generator=g)
+        t = timed(lambda: ops.segment_mean(fr, offs, perm), 200 if songs < 10_000 else 40)
+        report_fn(f"(f) segment mean {songs} songs x {fps} frames x {C} f64, permuted", F,
+                  F * (C * 8 + 8) + songs * C * 8, t)
 
 
 if __name__ == "__main__":
