@@ -9,7 +9,9 @@ from ._lib import CE_MAX_Q, CEError, load  # noqa: F401
 from .select import (MODES, ConsensusEntropySelector, committee_from_frames, select_queries,  # noqa: F401
                      song_groups, stack_committee)
 
-__all__ = ["select_queries", "ConsensusEntropySelector", "stack_committee", "committee_from_frames", "song_groups",
+from .session import SelectionSession  # noqa: F401,E402
+
+__all__ = ["SelectionSession", "select_queries", "ConsensusEntropySelector", "stack_committee", "committee_from_frames", "song_groups",
            "MODES", "CE_MAX_Q", "CEError", "load", "ops", "dist"]
 
 

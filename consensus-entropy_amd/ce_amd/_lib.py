@@ -43,6 +43,10 @@ SIGNATURES = {
     "ce_select_finish": (_int, [_i64, _i32, _vp, _sz, _vp, _vp, _vp]),
     "ce_select_finish_cands": (_int, [_i64, _i32, _vp, _sz, _vp, _vp]),
     "ce_merge_cands": (_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
+    "ce_excl_words": (_sz, [_i64]),
+    "ce_select_mc_excl": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _vp, _i32, _i64, _vp, _sz, _vp, _vp,
+                                 _vp]),
+    "ce_mark_selected": (_int, [_vp, _i64, _vp, _i32, _i64, _vp]),
     "ce_select_mix_workspace_bytes": (_sz, [_i64, _i64, _i32]),
     "ce_select_mix": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _sz,
                              _vp, _vp, _vp]),

@@ -179,16 +179,44 @@ def topq_merge(vals, idx, q):
     return ov, oi
 
 
-def select_mc(P, q, layout="MNC", base_idx=0):
-    """Fused amg_test.py:441-445: (vals [q], idx [q]) best-first."""
+def select_mc(P, q, layout="MNC", base_idx=0, excl=None):
+    """Fused amg_test.py:441-445: (vals [q], idx [q]) best-first.  excl: an
+    optional exclusion bitmap (int32 [ceil(N/32)], bit i set = item i is out
+    of the pool; q <= 64), see excl_bitmap / mark_selected."""
     N, M, C, sN, sM, sC, dt = committee_view(P, layout)
     q = _check_q(q)
     lib = _lib.load()
     ws = WORKSPACE.get(P.device, lib.ce_select_mc_workspace_bytes(N, q))
     vals, idx = _outs(q, P.device)
-    call("ce_select_mc", _p(P), dt, N, M, C, sN, sM, sC, q, int(base_idx), _p(ws), ws.numel(), _p(vals),
-         _p(idx), _stream(P.device))
+    if excl is None:
+        call("ce_select_mc", _p(P), dt, N, M, C, sN, sM, sC, q, int(base_idx), _p(ws), ws.numel(), _p(vals),
+             _p(idx), _stream(P.device))
+    else:
+        _check_excl(excl, N)
+        call("ce_select_mc_excl", _p(P), dt, N, M, C, sN, sM, sC, _p(excl), q, int(base_idx), _p(ws), ws.numel(),
+             _p(vals), _p(idx), _stream(P.device))
     return vals, idx
+
+
+def excl_bitmap(n, device=None):
+    """An all-clear exclusion bitmap for n items (int32 words on the device)."""
+    words = _lib.load().ce_excl_words(int(n))
+    return torch.zeros(max(int(words), 1), dtype=torch.int32, device=device)
+
+
+def _check_excl(excl, n):
+    _on_gpu(excl, "excl")
+    if excl.dtype != torch.int32 or not excl.is_contiguous() or excl.numel() * 32 < n:
+        raise ValueError(f"excl must be a contiguous int32 bitmap of >= {(n + 31) // 32} words")
+
+
+def mark_selected(excl, n, idx, base_idx=0):
+    """Set the bitmap bits of the selected positions idx (device int64; -1
+    slots ignored) -- stream-ordered after the selection that produced them."""
+    _check_excl(excl, n)
+    _on_gpu(idx, "idx")
+    idx = idx.to(torch.int64).contiguous()
+    call("ce_mark_selected", _p(excl), int(n), _p(idx), idx.numel(), int(base_idx), _stream(excl.device))
 
 
 class MCPlan:

@@ -1,0 +1,112 @@
+"""Device-resident multi-epoch selection.
+
+The reference shrinks its pools on the host every epoch: the queried songs
+leave X_train / id_tr (amg_test.py:521-531) and the hc frame
+(``this_consensus_hc[~index.isin(q_songs)]``, :455, :484), and the next epoch's
+``pred_prob`` is computed over what is left.  A ``SelectionSession`` keeps the
+FULL pool on the device instead, with one exclusion bitmap per pool: each
+epoch the caller hands in the committee's probabilities over the full pool
+(e.g. from on-device member inference), the engine selects among the items
+whose bit is clear, and marks the picks -- no pool bookkeeping crosses PCIe,
+only the q picked positions come back.
+
+Positions returned are positions in the FULL pool (stable across epochs), so
+the caller maps them to song ids once.  Selection per epoch equals the
+reference's on the shrunken pool (tests/test_gpu_parity.py::test_session_*).
+
+Modes (amg_test.py:425-489):
+  mc    committee over the full pool [M, N, C] (or [N, M, C]), excluding queried items
+  hc    the human-consensus table, fixed at construction, excluding queried rows
+  mix   both, ALIGNED pools (hc row r is mc item r, N_h == N): a pick through
+        either part removes the song from both, as :484 + :521-531 do by id;
+        positions in [0, 2N) index the row stack [mc; hc] like select_queries
+  rand  uniform among the remaining items with the caller's RandomState
+        (legacy np.random.shuffle of the remaining positions, first q)
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+from .select import MODES, _device, _hc_tensor, stack_committee
+
+
+class SelectionSession:
+    def __init__(self, queries, mode, n_items, *, hc=None, votes=None, rng=None, device=None, n_classes=4):
+        if mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}, got {mode!r}")
+        self.q = int(queries)
+        if not 1 <= self.q <= 64:
+            raise ValueError("a session selects 1..64 queries per epoch")
+        self.mode = mode
+        self.N = int(n_items)
+        self.dev = _device(device)
+        self.rng = rng
+        self.H = None
+        if mode in ("hc", "mix"):
+            self.H = _hc_tensor(hc, votes, n_classes, self.dev).to(torch.float64).contiguous()
+            if mode == "mix" and self.H.shape[0] != self.N:
+                raise ValueError("mix sessions need aligned pools: hc rows == n_items")
+            if mode == "hc":
+                self.N = self.H.shape[0]
+        self.excl = ops.excl_bitmap(self.N, self.dev)
+        self.n_selected = 0
+
+    @property
+    def remaining(self):
+        return self.N - self.n_selected
+
+    def _mc(self, committee, layout):
+        P, lay = stack_committee(committee, self.dev, layout)
+        n = P.shape[1] if lay == "MNC" else P.shape[0]
+        if n != self.N:
+            raise ValueError(f"committee covers {n} items, the session's pool has {self.N}")
+        return ops.select_mc(P, self.q, lay, excl=self.excl)
+
+    def _hc(self):
+        return ops.select_mc(self.H.unsqueeze(1), self.q, "NMC", excl=self.excl)
+
+    def select(self, committee=None, layout="MNC"):
+        """One epoch: returns the q picked positions (np.int64; fewer when the
+        pool runs dry) and removes them from the pool."""
+        q = self.q
+        if self.mode == "rand":
+            keep = ~self._mask()
+            pool = np.flatnonzero(keep).tolist()
+            (self.rng if self.rng is not None else np.random).shuffle(pool)
+            pick = np.asarray(pool[:q], np.int64)
+            ops.mark_selected(self.excl, self.N, torch.from_numpy(pick).to(self.dev))
+            self.n_selected += len(pick)
+            return pick
+        if self.mode == "mc":
+            if committee is None:
+                raise ValueError("mc mode needs `committee`")
+            _, idx = self._mc(committee, layout)
+            ops.mark_selected(self.excl, self.N, idx)
+        elif self.mode == "hc":
+            _, idx = self._hc()
+            ops.mark_selected(self.excl, self.N, idx)
+        else:  # mix: top-q of each part over the remaining songs, then the union's top-q
+            if committee is None:
+                raise ValueError("mix mode needs `committee`")
+            vm, im = self._mc(committee, layout)
+            vh, ih = self._hc()
+            ih = torch.where(ih >= 0, ih + self.N, ih)
+            _, idx = ops.topq_merge(torch.cat([vm, vh]), torch.cat([im, ih]), q)
+            # a song leaves both pools whichever part picked it (:484, :521-531)
+            song = torch.where(idx >= self.N, idx - self.N, idx)
+            ops.mark_selected(self.excl, self.N, song)
+        out = idx.cpu().numpy()
+        out = out[out >= 0]
+        if self.mode == "mix":
+            self.n_selected += len(np.unique(np.where(out >= self.N, out - self.N, out)))
+        else:
+            self.n_selected += len(out)
+        return out
+
+    def _mask(self):
+        """The exclusion bitmap as a host bool array [N] (True = queried)."""
+        words = self.excl.cpu().numpy().view(np.uint32)
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+        return bits[: self.N].astype(bool)

@@ -291,7 +291,9 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
             if (lane == j) mykey = order_key(h);
             if (j == 63 || ci == hi - 1) {
                 const int64_t t0 = ci - j;
-                tq.offer(mykey, t0 + lane + sa.base_idx, lane <= j);
+                bool ok = lane <= j;
+                if (sa.excl) ok = ok && !excluded(sa.excl, t0 + (lane <= j ? lane : j));
+                tq.offer(mykey, t0 + lane + sa.base_idx, ok);
                 mykey = 0;
             }
             ++ci;
@@ -1034,6 +1036,7 @@ static StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx) {
     s.base_idx = base_idx;
     s.nlists = G;
     s.per_wave = 0;
+    s.excl = nullptr;
     return s;
 }
 
@@ -1044,9 +1047,11 @@ static void stream_grid(StreamArgs& s, int grid) {
 }
 
 // Launches the streaming kernel when it applies; returns false otherwise.
-static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st) {
+static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
+                          const uint32_t* excl = nullptr) {
     if (!stream_enabled() || q > kStreamMaxQ || a.N == 0) return false;
     StreamArgs sa = stream_args(a, G, base_idx);
+    sa.excl = excl;
     const int eb = elem_bytes(a.dt);
     const int64_t R = (int64_t)a.M * a.C * eb;
     const bool dense_nmc = a.sC == 1 && a.sM == a.C && a.sN == (int64_t)a.M * a.C && (uintptr_t)a.p % 16 == 0;
@@ -1076,6 +1081,7 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
     const WideArgs wa = wide_args(a);
     const PwPlan pl = pw_plan(a.C);
     const size_t lds = wide_lds_bytes(a.C);
+    int rc_excl = CE_OK;
     rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
         constexpr int DT = decltype(dt)::value, NPL = decltype(npl)::value;
         if constexpr (decltype(vec)::value) {
@@ -1091,12 +1097,16 @@ static bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsL
                 return;
             }
         }
+        if (sa.excl) {  // k_stream_wide takes no bitmap
+            rc_excl = CE_EUNSUPPORTED;
+            return;
+        }
         auto kern = k_stream_wide<DT, NPL, decltype(vec)::value>;
         const int grid = resident_grid(kern, lds, G);
         stream_grid(sa, grid);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
     });
-    return rc == CE_OK;
+    return rc == CE_OK && rc_excl == CE_OK;
 }
 
 // Committee stage 1 for any supported shape: register path or wide path.
@@ -1194,6 +1204,23 @@ extern "C" int ce_segment_mean(const void* frames, ce_dtype dt, int64_t F, int32
     return check_launch("ce_segment_mean");
 }
 
+// ---- exclusion bitmaps (SelectionSession) -----------------------------------
+__global__ void k_mark(uint32_t* __restrict__ bits, int64_t N, const int64_t* __restrict__ idx, int n,
+                       int64_t base_idx) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const int64_t p = idx[t] - base_idx;
+        if (idx[t] >= 0 && p >= 0 && p < N) atomicOr(&bits[p >> 5], 1u << (p & 31));
+    }
+}
+
+extern "C" int ce_mark_selected(uint32_t* excl, int64_t N, const int64_t* idx, int32_t n, int64_t base_idx,
+                                ce_stream_t stream) {
+    if (N < 0 || n < 0 || (N > 0 && !excl) || (n > 0 && !idx)) return fail(CE_EINVAL, "bad mark arguments");
+    if (n == 0 || N == 0) return CE_OK;
+    hipLaunchKernelGGL(k_mark, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, excl, N, idx, n, base_idx);
+    return check_launch("ce_mark_selected");
+}
+
 // ---- top-q of an entropy vector -------------------------------------------
 extern "C" size_t ce_topq_workspace_bytes(int64_t N, int32_t q) {
     return lists_bytes(pool_blocks(N), q < 1 ? 1 : q);
@@ -1254,9 +1281,29 @@ static int mc_partial(const CommArgs& a, int q, int64_t base_idx, void* ws, size
     return CE_OK;
 }
 
+static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                          int64_t sC, const uint32_t* excl, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes,
+                          double* val_out, int64_t* idx_out, ce_stream_t stream);
+
 extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
                             int64_t sC, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes, double* val_out,
                             int64_t* idx_out, ce_stream_t stream) {
+    return select_mc_impl(p, dt, N, M, C, sN, sM, sC, nullptr, q, base_idx, ws, ws_bytes, val_out, idx_out, stream);
+}
+
+extern "C" size_t ce_excl_words(int64_t N) { return N > 0 ? (size_t)((N + 31) / 32) : 0; }
+
+extern "C" int ce_select_mc_excl(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                                 int64_t sM, int64_t sC, const uint32_t* excl, int32_t q, int64_t base_idx, void* ws,
+                                 size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    if (!excl && N > 0) return fail(CE_EINVAL, "null exclusion bitmap");
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "exclusion bitmaps need q <= %d (got %d)", kStreamMaxQ, q);
+    return select_mc_impl(p, dt, N, M, C, sN, sM, sC, excl, q, base_idx, ws, ws_bytes, val_out, idx_out, stream);
+}
+
+static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                          int64_t sC, const uint32_t* excl, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes,
+                          double* val_out, int64_t* idx_out, ce_stream_t stream) {
     if (!val_out || !idx_out) return fail(CE_EINVAL, "null output");
     hipStream_t st = (hipStream_t)stream;
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
@@ -1273,15 +1320,22 @@ extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, in
             using S = decltype(src);
             with_seg_batching<S>([&](auto unr, auto ipl) {
                 hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(1), dim3(64 * kSegWaves),
-                                   0, st, src, nullptr, N, base_idx, q, val_out, idx_out);
+                                   0, st, src, nullptr, N, base_idx, q, val_out, idx_out, excl);
             });
         });
         if (rc == CE_OK) return check_launch("ce_select_mc");
     }
     int G = 0;
     bool fin = false;
-    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, &fin, st);
-    if (rc) return rc;
+    int rc;
+    if (excl) {  // the streaming engine only (the q > 64 paths take no bitmap)
+        G = pool_blocks(N);
+        if (!stream_enabled() || !wide2_enabled() || !launch_stream(a, G, q, base_idx, carve(ws, G, q), st, excl))
+            return fail(CE_EUNSUPPORTED, "exclusion bitmap: no streaming kernel for this shape");
+    } else {
+        rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, &fin, st);
+        if (rc) return rc;
+    }
     if (!fin) finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
     return check_launch("ce_select_mc");
 }
@@ -1412,7 +1466,8 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
             using S = decltype(src);
             with_seg_batching<S>([&](auto unr, auto ipl) {
                 hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(U), dim3(64 * user_waves(total_items, U)),
-                                   0, st, src, offsets, (int64_t)0, (int64_t)0, q, val_out, idx_out);
+                                   0, st, src, offsets, (int64_t)0, (int64_t)0, q, val_out, idx_out,
+                                   (const uint32_t*)nullptr);
             });
         });
         if (rc == CE_OK) return check_launch("ce_select_batched");

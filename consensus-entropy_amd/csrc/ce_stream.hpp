@@ -87,6 +87,9 @@ __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t b
     for (int j = 32; j > 0; j >>= 1) cx_stage(k, i, j, true);
 }
 
+// bit i of an exclusion bitmap (SelectionSession: items already queried)
+__device__ __forceinline__ bool excluded(const uint32_t* b, int64_t i) { return (b[i >> 5] >> (i & 31)) & 1u; }
+
 struct RegTopQ {
     uint64_t k;   // this lane's slot
     int64_t i;
@@ -255,6 +258,7 @@ struct StreamArgs {
     bool pow2;
     int64_t base_idx;
     int64_t per_wave;  // items per wave (multiple of 64)
+    const uint32_t* excl;  // exclusion bitmap over items 0..N-1 (1 = out of the pool), or nullptr
     int nlists;        // workspace lists (>= gridDim.x); lists past the grid are written empty
 };
 
@@ -331,7 +335,9 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
         t.template mean<DT, C>(a.dM, a.invM, a.pow2, mean);
         const double h = entropy_row<C>(mean);
         const int64_t i = t0 + lane;
-        tq.offer(order_key(h), i + a.base_idx, i < hi);
+        bool ok = i < hi;
+        if (a.excl) ok = ok && !excluded(a.excl, i < hi ? i : hi - 1);
+        tq.offer(order_key(h), i + a.base_idx, ok);
     }
     block_merge_write<4>(tq, sm.lists, q, wc + (int64_t)blockIdx.x * q, a.nlists);
 }
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
 // member loads in flight per lane.
 template <class Src, int IPL, int UNR>
 __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, int64_t hi, int64_t rel, int q,
-                                                    RegTopQ& tq) {
+                                                    RegTopQ& tq, const uint32_t* excl = nullptr) {
     const int lane = threadIdx.x & 63;
     for (int64_t t0 = lo; t0 < hi; t0 += 64 * IPL) {
         uint64_t k[IPL];
@@ -355,7 +361,9 @@ __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, 
 #pragma unroll
         for (int u = 0; u < IPL; ++u) {
             const int64_t i = t0 + 64 * u + lane;
-            tq.offer(k[u], i + rel, i < hi);
+            bool ok = i < hi;
+            if (excl) ok = ok && !excluded(excl, items[u]);  // items[u]: i clamped into the pool
+            tq.offer(k[u], i + rel, ok);
         }
     }
 }
@@ -371,7 +379,7 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     if (lo > hi) lo = hi;
     RegTopQ tq;
     tq.init(q);
-    stream_direct_range<Src, IPL, UNR>(src, lo, hi, a.base_idx, q, tq);
+    stream_direct_range<Src, IPL, UNR>(src, lo, hi, a.base_idx, q, tq, a.excl);
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists);
 }
 
@@ -383,8 +391,10 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
 template <class Src, int IPL, int UNR, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int64_t n,
                                                             int64_t base_idx, int q, double* __restrict__ oval,
-                                                            int64_t* __restrict__ oidx) {
+                                                            int64_t* __restrict__ oidx,
+                                                            const uint32_t* __restrict__ excl) {
     // launched with WAVES or fewer waves (a power of two): blockDim.x / 64
+    // excl: exclusion bitmap over the tensor's items, or nullptr
     __shared__ WaveListsT<WAVES> sm;
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int64_t s0 = offsets ? offsets[blockIdx.x] : 0, s1 = offsets ? offsets[blockIdx.x + 1] : n;
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_
     if (lo > hi) lo = hi;
     RegTopQ tq;
     tq.init(q);
-    stream_direct_range<Src, IPL, UNR>(src, lo, hi, (offsets ? 0 : base_idx) - s0, q, tq);
+    stream_direct_range<Src, IPL, UNR>(src, lo, hi, (offsets ? 0 : base_idx) - s0, q, tq, excl);
     const int64_t slot = (int64_t)blockIdx.x * q;
     block_merge_write<WAVES>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot, nw);
 }

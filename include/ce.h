@@ -164,6 +164,25 @@ int ce_merge_cands(const ce_cand *c, int32_t nlists, int32_t q, double *val_out,
                    ce_stream_t stream);
 
 /*
+ * Device-resident multi-epoch selection (amg_test.py:396-397
+ * epochs, :455/:484 hc-pool shrink, :521-531 X_train shrink): instead of
+ * rebuilding the pool every epoch, the caller keeps the full pool on the device
+ * with an exclusion bitmap (bit i of word i/32 set = item i already queried).
+ *   ce_excl_words      uint32 words of a bitmap for N items (host arithmetic)
+ *   ce_select_mc_excl  ce_select_mc over the items whose bit is clear (q <= 64)
+ *   ce_mark_selected   set the bits of the n positions idx[0..n) (minus
+ *                      base_idx; negative / out-of-range entries ignored) --
+ *                      fed the previous call's idx_out, nothing leaves the GPU
+ */
+size_t ce_excl_words(int64_t N);
+int ce_select_mc_excl(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                      int64_t sM, int64_t sC, const uint32_t *excl, int32_t q, int64_t base_idx,
+                      void *ws, size_t ws_bytes, double *val_out, int64_t *idx_out,
+                      ce_stream_t stream);
+int ce_mark_selected(uint32_t *excl, int64_t N, const int64_t *idx, int32_t n, int64_t base_idx,
+                     ce_stream_t stream);
+
+/*
  * Fused mix selection -- replaces amg_test.py:473-480: the ROW stack
  * [mc consensus (N rows); hc table (N_h rows)], entropy, top-q over the union.
  * Positions in [0, N) are committee items, [N, N + N_h) hc rows.

@@ -420,3 +420,73 @@ def test_frames_to_selection(ce):
     assert np.array_equal(stack.cpu().numpy(), P)
     _, idx = ce.ops.select_mc(stack, 10, "MNC")
     assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, 10, "MNC")[1])
+
+
+def _shrinking_reference(mode, epochs, q, committees, hc):
+    """The reference's epoch loop on the host: pools shrink by the picks
+    (amg_test.py:455, :484, :521-531) and every epoch selects on what is left
+    (oracle arithmetic); picks are reported as positions of the full pool."""
+    from oracle import ce_oracle as O
+
+    N = committees[0].shape[1] if committees else hc.shape[0]
+    alive = np.ones(N, bool)
+    out = []
+    for e in range(epochs):
+        pos = np.flatnonzero(alive)
+        if mode == "mc":
+            _, i = O.oracle_select_mc(committees[e][:, pos], q, "MNC")
+            picks = pos[i]
+            songs = picks
+        elif mode == "hc":
+            _, i = O.oracle_topq(O.oracle_table_entropy(hc[pos]), q)
+            picks = pos[i]
+            songs = picks
+        else:
+            ent = np.concatenate([O.oracle_committee_entropy(committees[e][:, pos], "MNC"),
+                                  O.oracle_table_entropy(hc[pos])])
+            _, i = O.oracle_topq(ent, q)
+            n = len(pos)
+            picks = np.where(i < n, pos[np.minimum(i, n - 1)], N + pos[np.maximum(i - n, 0)])
+            songs = np.where(picks >= N, picks - N, picks)
+        alive[songs] = False
+        out.append(np.asarray(picks, np.int64))
+    return out
+
+
+@pytest.mark.parametrize("mode", ["mc", "hc", "mix"])
+def test_session_equals_shrinking_pools(ce, mode):
+    """SelectionSession (full pool on the device + exclusion bitmap) selects,
+    epoch after epoch, exactly what the reference's shrinking-pool loop does."""
+    rng = np.random.default_rng(len(mode))
+    N, q, epochs = 3000, 10, 6
+    committees = [np.floor(synth(rng, N, 4, 4, np.float64) * 64).transpose(1, 0, 2) / 64 + 1e-3
+                  for _ in range(epochs)]  # coarse: ties across the shrinking pool
+    hc = np.round(rng.dirichlet(np.ones(4), N), 3)
+    hc[::7] = hc[3]  # exact ties in the table
+    exp = _shrinking_reference(mode, epochs, q, committees, hc)
+    sess = ce.SelectionSession(q, mode, N, hc=hc if mode != "mc" else None)
+    for e in range(epochs):
+        got = sess.select(committee=dev(committees[e]) if mode != "hc" else None)
+        assert np.array_equal(got, exp[e]), (mode, e, got, exp[e])
+    assert sess.remaining == N - len(np.unique(np.concatenate(
+        [np.where(x >= N, x - N, x) for x in exp])))
+
+
+def test_session_rand_and_exhaustion(ce):
+    """rand draws only remaining items; a pool smaller than q*epochs runs dry
+    without repeats; the exclusion API rejects q > 64."""
+    N, q = 45, 10
+    sess = ce.SelectionSession(q, "rand", N, rng=np.random.RandomState(1987))
+    seen = []
+    for _ in range(5):
+        seen.extend(sess.select().tolist())
+    assert sorted(seen) == list(range(N)) and sess.remaining == 0
+    assert len(sess.select()) == 0
+    P = dev(np.full((2, 100, 4), 0.25))
+    ex = ce.ops.excl_bitmap(100, "cuda")
+    with pytest.raises(Exception):
+        ce.ops.select_mc(P, 65, excl=ex)
+    sess = ce.SelectionSession(4, "mc", 100)
+    for _ in range(25):
+        sess.select(committee=P)
+    assert sess.remaining == 0 and len(sess.select(committee=P)) == 0
