@@ -17,7 +17,8 @@ except ImportError:  # pragma: no cover - torch is part of this image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libce_amd.so")
+# CE_AMD_LIB: an alternative build of the same ABI (A/B runs of kernel variants)
+LIB_PATH = os.environ.get("CE_AMD_LIB") or os.path.join(_HERE, "libce_amd.so")
 
 CE_OK, CE_EINVAL, CE_EWORKSPACE, CE_ELAUNCH, CE_EUNSUPPORTED = 0, -1, -2, -3, -4
 CE_F32, CE_F64, CE_BF16 = 0, 1, 2

@@ -50,14 +50,55 @@ __device__ __forceinline__ void shfl_cand(uint64_t& k, int64_t& i, int src) {
     i = (int64_t)(((uint64_t)i1 << 32) | i0);
 }
 
+// Lane exchange "value of lane ^ J" without the LDS crossbar (ds_bpermute
+// throughput, not latency, bounded the sort networks): DPP quad_perm for J =
+// 1, 2; row_half_mirror (lane ^ 7) then quad reverse (lane ^ 3) for J = 4;
+// row_ror:8 for J = 8; the gfx950 permlane16/32 swaps for J = 16, 32.
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (J == 4) {
+        const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, t, 0x1B, 0xF, 0xF, false);      // quad_perm [3,2,1,0]
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    } else if constexpr (J == 16) {
+        const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (threadIdx.x & 16) ? p[0] : p[1];
+    } else {
+        static_assert(J == 32, "lane exchange distance");
+        const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (threadIdx.x & 32) ? p[0] : p[1];
+    }
+}
+
+// value of lane - 1 (DPP wave_shr:1)
+__device__ __forceinline__ uint64_t lane_above(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int J>
+__device__ __forceinline__ void xor_cand(uint64_t& k, int64_t& i) {
+    const uint32_t k0 = xor_lane<J>((uint32_t)k), k1 = xor_lane<J>((uint32_t)(k >> 32));
+    const uint32_t i0 = xor_lane<J>((uint32_t)(uint64_t)i), i1 = xor_lane<J>((uint32_t)((uint64_t)i >> 32));
+    k = ((uint64_t)k1 << 32) | k0;
+    i = (int64_t)(((uint64_t)i1 << 32) | i0);
+}
+
 // One compare-exchange stage of a bitonic network across the wave: partner
-// lane ^ j; `desc` = this lane's block sorts best-first.
-__device__ __forceinline__ void cx_stage(uint64_t& k, int64_t& i, int j, bool desc) {
+// lane ^ J; `desc` = this lane's block sorts best-first.
+template <int J>
+__device__ __forceinline__ void cx_stage(uint64_t& k, int64_t& i, bool desc) {
     const int lane = threadIdx.x & 63;
     uint64_t pk = k;
     int64_t pi = i;
-    shfl_cand(pk, pi, lane ^ j);
-    const bool lower = (lane & j) == 0;
+    xor_cand<J>(pk, pi);
+    const bool lower = (lane & J) == 0;
     const bool pb = better(pk, pi, k, i);
     const bool take = (lower == desc) ? pb : !pb;
     if (take) {
@@ -66,14 +107,20 @@ __device__ __forceinline__ void cx_stage(uint64_t& k, int64_t& i, int j, bool de
     }
 }
 
-// Sort the wave's 64 (k, i) best-first.
-__device__ __forceinline__ void wave_sort64(uint64_t& k, int64_t& i) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int s = 2; s <= 64; s <<= 1)
-#pragma unroll
-        for (int j = s >> 1; j > 0; j >>= 1) cx_stage(k, i, j, (lane & s) == 0);
+template <int S, int J>
+__device__ __forceinline__ void sort_stages(uint64_t& k, int64_t& i) {
+    cx_stage<J>(k, i, ((threadIdx.x & 63) & S) == 0);
+    if constexpr (J > 1) sort_stages<S, J / 2>(k, i);
 }
+
+template <int S>
+__device__ __forceinline__ void sort_levels(uint64_t& k, int64_t& i) {
+    sort_stages<S, S / 2>(k, i);
+    if constexpr (S < 64) sort_levels<S * 2>(k, i);
+}
+
+// Sort the wave's 64 (k, i) best-first (21 stages).
+__device__ __forceinline__ void wave_sort64(uint64_t& k, int64_t& i) { sort_levels<2>(k, i); }
 
 // (k, i) := best 64 of the two best-first lists (k, i) and (bk, bi), best-first.
 __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t bk, int64_t bi) {
@@ -83,8 +130,7 @@ __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t b
         k = bk;
         i = bi;
     }
-#pragma unroll
-    for (int j = 32; j > 0; j >>= 1) cx_stage(k, i, j, true);
+    sort_stages<64, 32>(k, i);  // half-cleaners 32 .. 1, all best-first
 }
 
 // bit i of an exclusion bitmap (SelectionSession: items already queried)
@@ -123,9 +169,8 @@ struct RegTopQ {
         const int lane = threadIdx.x & 63;
         const uint64_t below = __ballot(better(ck, ci, k, i));  // slots the candidate beats: a suffix
         const int p = __builtin_ctzll(below);
-        uint64_t uk = k;
-        int64_t ui = i;
-        shfl_cand(uk, ui, lane > 0 ? lane - 1 : 0);
+        const uint64_t uk = lane_above(k);  // lane 0 never takes it
+        const int64_t ui = (int64_t)lane_above((uint64_t)i);
         if (lane > p) {
             k = uk;
             i = ui;
