@@ -30,7 +30,6 @@ namespace ce {
 
 constexpr int kBS = 256;          // stage-1 block: 4 waves
 constexpr int kFinBS = 1024;      // stage-2 block: 16 waves
-constexpr int kMinRounds = 4;     // >= 4 rounds of kBS items per stage-1 block (batched split)
 constexpr int kMinItemsPerBlock = 64;
 constexpr int64_t kSmallPoolBytes = 256 * 1024;  // below this one block does the whole selection
 constexpr int kMaxBlocks = 1024;  // stage-1 blocks per pool (4 per CU on 256 CUs)
@@ -588,6 +587,30 @@ __global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int 
         block_merge_write<16>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot);
 }
 
+// Per-segment merge of a few lists (batched users: bpu lists of q each): one
+// wave per segment streams its nl*q candidates through a register top-q.
+template <bool FROM_VALS>
+__global__ __launch_bounds__(256) void k_merge_wave(ListSrc<FROM_VALS> src, int segs, int nl, int q,
+                                                    double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    const int seg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (seg >= segs) return;  // wave-uniform; no block barrier below
+    const int64_t L = (int64_t)nl * q, seg0 = (int64_t)seg * L;
+    RegTopQ tq;
+    tq.init(q);
+    for (int64_t c0 = 0; c0 < L; c0 += 64) {
+        const int64_t j = c0 + lane;
+        uint64_t k;
+        int64_t id;
+        src.get(seg0 + (j < L ? j : L - 1), k, id);
+        tq.offer(k, id, j < L && id >= 0);
+    }
+    if (lane < q) {
+        const bool ok = tq.i != INT64_MAX;
+        oval[(int64_t)seg * q + lane] = ok ? key_to_val(tq.k) : __longlong_as_double(0x7ff8000000000000ll);
+        oidx[(int64_t)seg * q + lane] = ok ? tq.i : -1;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Per-item entropy to HBM.
 // ---------------------------------------------------------------------------
@@ -984,13 +1007,6 @@ static void with_batching(int M, F&& f) {
     }
 }
 
-// Waves per user block of ce_select_batched: 8 for many users (two 8-wave
-// blocks per CU keep ~512 users resident at once), 16 for a few large ones.
-static int user_waves(int64_t total, int U) {
-    const int64_t avg = total / (U > 0 ? U : 1);
-    return (U >= 256 || avg < 4096) ? 8 : 16;
-}
-
 // The same for k_stream_seg: up to 16-wave blocks (<= 128 VGPRs), so fewer loads per lane.
 template <class Src, class F>
 static void with_seg_batching(F&& f) {
@@ -1315,15 +1331,23 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
     if (!ws || ws_bytes < lists_bytes(pool_blocks(N), q)) return fail(CE_EWORKSPACE, "workspace too small");
     if (stream_enabled() && q <= kStreamMaxQ && N > 0 &&
         N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes) {
-        // small pool: one block scores and selects, one launch, no workspace traffic
+        // small pool: ~512 items per 4-wave block on a few CUs (one block: it
+        // is the final answer), then one wave merges the blocks' lists
+        const int nb = (int)std::min<int64_t>(std::min<int64_t>(cdiv(N, 512), 32), pool_blocks(N));
+        WsLists w = carve(ws, nb, q);
         const int rc = with_committee(a, [&](auto src) {
             using S = decltype(src);
             with_seg_batching<S>([&](auto unr, auto ipl) {
-                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(1), dim3(64 * kSegWaves),
-                                   0, st, src, nullptr, N, base_idx, q, val_out, idx_out, excl);
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(nb),
+                                   dim3(256), 0, st, src, nullptr, N, base_idx, q, nb, val_out, idx_out, w.c, excl);
             });
         });
-        if (rc == CE_OK) return check_launch("ce_select_mc");
+        if (rc == CE_OK) {
+            if (nb > 1)
+                hipLaunchKernelGGL((k_merge_wave<false>), dim3(1), dim3(256), 0, st, ListSrc<false>{w.c, nullptr, nullptr},
+                                   1, nb, q, val_out, idx_out);
+            return check_launch("ce_select_mc");
+        }
     }
     int G = 0;
     bool fin = false;
@@ -1434,11 +1458,13 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
 }
 
 // ---- batched users -------------------------------------------------------------
+// blocks per user: ~512 items per block (one iteration per wave of a 4-wave
+// block), at most ~4096 blocks in all
 static int batched_bpu(int64_t total, int U) {
     if (U < 1) return 1;
     const int64_t avg = cdiv(total, U);
-    int64_t bpu = cdiv(avg, (int64_t)kBS * kMinRounds);
-    const int64_t cap = std::max<int64_t>(1, 2048 / U);
+    int64_t bpu = cdiv(avg, (int64_t)512);
+    const int64_t cap = std::max<int64_t>(1, 4096 / U);
     bpu = std::max<int64_t>(1, std::min(bpu, cap));
     return (int)bpu;
 }
@@ -1461,18 +1487,24 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     const int64_t nl = (int64_t)bpu * U;
     if (!ws || ws_bytes < lists_bytes(nl, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, nl, q);
     if (stream_enabled() && q <= kStreamMaxQ) {
+        // bpu 4-wave blocks per user, then one wave per user merges its bpu lists
         rc = with_committee(a, [&](auto src) {
             using S = decltype(src);
             with_seg_batching<S>([&](auto unr, auto ipl) {
-                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(U), dim3(64 * user_waves(total_items, U)),
-                                   0, st, src, offsets, (int64_t)0, (int64_t)0, q, val_out, idx_out,
-                                   (const uint32_t*)nullptr);
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>),
+                                   dim3((unsigned)nl), dim3(bpu == 1 ? 64 * kSegWaves : 256), 0, st, src, offsets,
+                                   (int64_t)0, (int64_t)0, q, bpu, val_out, idx_out, w.c, (const uint32_t*)nullptr);
             });
         });
-        if (rc == CE_OK) return check_launch("ce_select_batched");
+        if (rc == CE_OK) {
+            if (bpu > 1)
+                hipLaunchKernelGGL((k_merge_wave<false>), dim3((U + 3) / 4), dim3(256), 0, st,
+                                   ListSrc<false>{w.c, nullptr, nullptr}, U, bpu, q, val_out, idx_out);
+            return check_launch("ce_select_batched");
+        }
     }
-    WsLists w = carve(ws, nl, q);
     Seg sg{offsets, total_items, bpu, 0};
     const bool fin = bpu == 1;
     rc = committee_partial(a, sg, (int)nl, q, w, val_out, idx_out, fin, st);

@@ -119,6 +119,36 @@ __device__ __forceinline__ void sort_levels(uint64_t& k, int64_t& i) {
     if constexpr (S < 64) sort_levels<S * 2>(k, i);
 }
 
+// The wave's best (k, i) in every lane (6 butterfly stages).
+template <int J>
+__device__ __forceinline__ void best_stages(uint64_t& k, int64_t& i) {
+    uint64_t pk = k;
+    int64_t pi = i;
+    xor_cand<J>(pk, pi);
+    if (better(pk, pi, k, i)) {
+        k = pk;
+        i = pi;
+    }
+    if constexpr (J < 32) best_stages<J * 2>(k, i);
+}
+__device__ __forceinline__ void wave_best64(uint64_t& k, int64_t& i) { best_stages<1>(k, i); }
+
+// Each 16-lane row's best (k, i) in all its lanes (4 butterfly stages).
+__device__ __forceinline__ void row_best16(uint64_t& k, int64_t& i) {
+    uint64_t pk;
+    int64_t pi;
+#define CE_RB(J)                          \
+    pk = k;                               \
+    pi = i;                               \
+    xor_cand<J>(pk, pi);                  \
+    if (better(pk, pi, k, i)) {           \
+        k = pk;                           \
+        i = pi;                           \
+    }
+    CE_RB(1) CE_RB(2) CE_RB(4) CE_RB(8)
+#undef CE_RB
+}
+
 // Sort the wave's 64 (k, i) best-first (21 stages).
 __device__ __forceinline__ void wave_sort64(uint64_t& k, int64_t& i) { sort_levels<2>(k, i); }
 
@@ -428,32 +458,106 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists);
 }
 
-// Batched pools (amg_test.py:345's per-user loop in one launch): block u owns
-// segment [offsets[u], offsets[u+1]), its WAVES waves split it in whole
-// iterations of 64*IPL items, and the block's merged top-q is the user's final
-// answer (user-local positions).  offsets == nullptr: one segment [0, n) with
-// positions base_idx + i (the single-launch path for small pools).
+// Batched pools (amg_test.py:345's per-user loop in one launch): user u owns
+// segment [offsets[u], offsets[u+1]), split over bpu consecutive blocks (block
+// b: user b / bpu, part b % bpu) in whole iterations of 64*IPL items; the
+// block's waves split its part the same way.  bpu == 1: the block's merged
+// top-q is the user's final answer (oval/oidx, user-local positions); bpu > 1:
+// the block writes its list to wc[b*q ..] for a per-user merge.
+// offsets == nullptr: one segment [0, n) with positions base_idx + i (the
+// single-launch path for small pools).  excl: exclusion bitmap over the
+// tensor's items, or nullptr.  Launched with WAVES or fewer waves (a power of two).
 template <class Src, int IPL, int UNR, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_t* __restrict__ offsets, int64_t n,
-                                                            int64_t base_idx, int q, double* __restrict__ oval,
-                                                            int64_t* __restrict__ oidx,
-                                                            const uint32_t* __restrict__ excl) {
-    // launched with WAVES or fewer waves (a power of two): blockDim.x / 64
-    // excl: exclusion bitmap over the tensor's items, or nullptr
+                                                            int64_t base_idx, int q, int bpu,
+                                                            double* __restrict__ oval, int64_t* __restrict__ oidx,
+                                                            Cand* __restrict__ wc, const uint32_t* __restrict__ excl) {
     __shared__ WaveListsT<WAVES> sm;
-    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int64_t s0 = offsets ? offsets[blockIdx.x] : 0, s1 = offsets ? offsets[blockIdx.x + 1] : n;
+    __shared__ uint64_t fk_s[4 * WAVES];
+    __shared__ int64_t fi_s[4 * WAVES];
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+    const int u = blockIdx.x / bpu, part = blockIdx.x % bpu;
+    const int64_t s0 = offsets ? offsets[u] : 0, s1 = offsets ? offsets[u + 1] : n;
     const int64_t len = s1 > s0 ? s1 - s0 : 0;
     constexpr int64_t kIt = 64 * IPL;
-    const int64_t per = ((len + kIt - 1) / kIt + nw - 1) / nw * kIt;
-    int64_t lo = s0 + w * per;
-    int64_t hi = lo + per < s1 ? lo + per : s1;
+    const int64_t its = (len + kIt - 1) / kIt;                  // iterations of the segment
+    const int64_t its_b = (its + bpu - 1) / bpu;                // per block
+    const int64_t its_w = (its_b + nw - 1) / nw;                // per wave
+    int64_t lo = s0 + ((int64_t)part * its_b + (int64_t)w * its_w) * kIt;
+    int64_t hi_b = s0 + ((int64_t)part + 1) * its_b * kIt;      // this block's end
+    if (hi_b > s1) hi_b = s1;
+    int64_t hi = lo + its_w * kIt < hi_b ? lo + its_w * kIt : hi_b;
     if (lo > hi) lo = hi;
+    const int64_t rel = (offsets ? 0 : base_idx) - s0;
+    // First iteration's keys, then a block-wide floor before any offer: the
+    // best of each 16-lane row is a distinct item, so the q-th best of the
+    // block's 4*nw row bests is an exact lower bound (q items of the block's
+    // part are >= it).  Most candidates then fail the first ballot and the
+    // sort networks a cold wave list would run on every early batch are skipped.
+    uint64_t k0[IPL];
+    int64_t it0[IPL];
+    bool ok0[IPL];
+#pragma unroll
+    for (int v = 0; v < IPL; ++v) {
+        const int64_t i = lo + 64 * v + lane;
+        it0[v] = i < hi ? i : hi - 1;
+        ok0[v] = false;
+        k0[v] = 0;
+    }
+    if (lo < hi) {  // wave-uniform
+        src.template keys<UNR, IPL>(it0, k0);
+#pragma unroll
+        for (int v = 0; v < IPL; ++v) {
+            ok0[v] = lo + 64 * v + lane < hi;
+            if (excl) ok0[v] = ok0[v] && !excluded(excl, it0[v]);
+        }
+    }
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+#pragma unroll
+    for (int v = 0; v < IPL; ++v)
+        if (ok0[v] && better(k0[v], lo + 64 * v + lane + rel, bk, bi)) {
+            bk = k0[v];
+            bi = lo + 64 * v + lane + rel;
+        }
+    row_best16(bk, bi);
+    if ((lane & 15) == 0) {
+        fk_s[w * 4 + (lane >> 4)] = bk;
+        fi_s[w * 4 + (lane >> 4)] = bi;
+    }
+    __syncthreads();
+    uint64_t fk = 0;
+    int64_t fi = INT64_MAX;
+    const int nb = 4 * nw;
+    if (q <= nb) {
+        bool hit = false;
+        uint64_t vk = 0;
+        int64_t vi = INT64_MAX;
+        if (lane < nb) {
+            vk = fk_s[lane];
+            vi = fi_s[lane];
+            int rank = 0;
+            for (int v = 0; v < nb; ++v) rank += better(fk_s[v], fi_s[v], vk, vi);
+            hit = vi != INT64_MAX && rank == q - 1;
+        }
+        const uint64_t m = __ballot(hit);
+        if (m) {
+            const int sl = __builtin_ctzll(m);
+            fk = readlane64(vk, sl);
+            fi = (int64_t)readlane64((uint64_t)vi, sl) + 1;  // admit candidates >= the bound
+        }
+    }
     RegTopQ tq;
-    tq.init(q);
-    stream_direct_range<Src, IPL, UNR>(src, lo, hi, (offsets ? 0 : base_idx) - s0, q, tq, excl);
-    const int64_t slot = (int64_t)blockIdx.x * q;
-    block_merge_write<WAVES>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot, nw);
+    tq.init(q, fk, fi);
+#pragma unroll
+    for (int v = 0; v < IPL; ++v) tq.offer(k0[v], lo + 64 * v + lane + rel, ok0[v]);
+    if (lo + kIt < hi) stream_direct_range<Src, IPL, UNR>(src, lo + kIt, hi, rel, q, tq, excl);
+    if (bpu == 1) {
+        const int64_t slot = (int64_t)u * q;
+        block_merge_write<WAVES>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot, nw);
+    } else {
+        block_merge_write<WAVES>(tq, sm, q, wc + (int64_t)blockIdx.x * q, 0, nullptr, nullptr, nw);
+    }
 }
 
 }  // namespace ce
