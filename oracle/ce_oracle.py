@@ -44,6 +44,29 @@ def ref_mc(pred_prob, q):
     return q_ind, ent, consensus_prob
 
 
+def ref_mc_shard_time(args):
+    """One worker of bench.py's multi-core CPU baseline: builds its own shard
+    of a mixed f64/f32 committee (seeded) and times ref_mc on it (median of
+    `reps` after a warm-up), single-threaded.  Returns (seconds, items)."""
+    import statistics
+    import time
+
+    n, M, C, q, seed, reps = args
+    rng = np.random.default_rng(seed)
+    members = []
+    for m in range(M):
+        e = -np.log(rng.random((n, C)))
+        p = e / e.sum(-1, keepdims=True)
+        members.append(p if m < M // 2 else p.astype(np.float32))
+    ref_mc(members, q)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ref_mc(members, q)
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), n
+
+
 def ref_hc(consensus_hc, q):
     """amg_test.py:451-452 verbatim on an [N_h, C] frequency table."""
     from scipy.stats import entropy
