@@ -271,9 +271,15 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     // issue cursor (item, batch) and consume cursor
     int64_t ii = lo, ci = lo;
     int ib = 0, cb = 0;
+    uint32_t off[KCH];  // this lane's chunk offsets in a member row (clamped into the row)
+#pragma unroll
+    for (int kk = 0; kk < KCH; ++kk) {
+        const int ch = lane + 64 * kk;
+        off[kk] = 16u * (uint32_t)(ch < K ? ch : K - 1);
+    }
     WideBatch<DT, KCH, UNR> A, B;
     auto issue = [&](WideBatch<DT, KCH, UNR>& X) {
-        X.issue(base + ii * sNb, ib * UNR, sMb, K);
+        X.issue(base + ii * sNb, ib * UNR, sMb, off);
         if (++ib == NB) {
             ib = 0;
             ++ii;

@@ -294,17 +294,19 @@ template <int DT, int KCH, int UNR>
 struct WideBatch {
     uint32_t v[UNR][KCH][4];
 
-    __device__ __forceinline__ void issue(const char* item, int m0, int64_t sMb, int K) {
+    // item/m0 are wave-uniform: the member row base is made a scalar (readfirstlane)
+    // so each load is SGPR base + the lane's constant 32-bit chunk offset (off[kk])
+    __device__ __forceinline__ void issue(const char* item, int m0, int64_t sMb, const uint32_t (&off)[KCH]) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
+            const uint64_t rb = (uint64_t)(item + (int64_t)(m0 + u) * sMb);
+            const char* row = reinterpret_cast<const char*>(
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rb >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rb));
 #pragma unroll
             for (int kk = 0; kk < KCH; ++kk) {
-                const int ch = lane + 64 * kk;
-                const int chs = ch < K ? ch : K - 1;
-                const u32x4 x =
-                    __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(item + (int64_t)(m0 + u) * sMb) + chs);
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + off[kk]));
                 v[u][kk][0] = x.x;
                 v[u][kk][1] = x.y;
                 v[u][kk][2] = x.z;

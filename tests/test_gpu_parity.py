@@ -490,3 +490,23 @@ def test_session_rand_and_exhaustion(ce):
     for _ in range(25):
         sess.select(committee=P)
     assert sess.remaining == 0 and len(sess.select(committee=P)) == 0
+
+
+@pytest.mark.parametrize("N,M,C,dt", [(2_000_000, 16, 4, np.float32), (1_000_000, 4, 4, np.float64),
+                                      (20_000, 3, 1000, np.float32)])
+def test_entropy_ulp_distribution(ce, N, M, C, dt):
+    """DESIGN.md 'Numerics': every sum is in numpy's order, so device and glibc
+    entropies differ only through log -- by at most 2 ulp, and the vast
+    majority are bit-identical (the fraction is printed)."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(11)
+    e = -np.log(rng.random((N, M, C)))
+    P = (e / e.sum(-1, keepdims=True)).astype(dt)
+    g = ce.ops.committee_entropy(dev(P), "NMC").cpu().numpy()
+    o = O.oracle_committee_entropy(P, "NMC")
+    ulp = np.abs(g.view(np.int64) - o.view(np.int64))
+    print(f"N={N} M={M} C={C} {np.dtype(dt).name}: exact {np.mean(ulp == 0):.6f} max ulp {ulp.max()} "
+          f"hist {np.bincount(np.minimum(ulp, 5)).tolist()}")
+    assert ulp.max() <= 2
+    assert np.mean(ulp == 0) > 0.95
