@@ -510,3 +510,29 @@ def test_entropy_ulp_distribution(ce, N, M, C, dt):
           f"hist {np.bincount(np.minimum(ulp, 5)).tolist()}")
     assert ulp.max() <= 4
     assert np.mean(ulp == 0) > 0.9
+
+
+def test_randomised_selection_fuzz(ce):
+    """Seeded fuzz of the whole selection path against the oracle: random pool
+    sizes (single-block, split small-pool, multi-block streaming), q in 1..64,
+    member counts, layouts and dtypes, with NaN rows, exact ties, -0.0 and
+    all-zero rows sprinkled in."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(20261016)
+    for case in range(40):
+        N = int(rng.choice([1, 2, 63, 65, 500, 1608, 5000, 70_000, 300_000]))
+        M = int(rng.choice([1, 2, 3, 4, 7, 16]))
+        C = int(rng.choice([2, 3, 4, 8]))
+        q = int(rng.integers(1, 65))
+        dt = [np.float32, np.float64][int(rng.integers(0, 2))]
+        P = synth(rng, N, M, C, np.float64, quant=int(rng.choice([0, 4, 16])) or None).astype(dt)
+        if N > 10:
+            P[rng.integers(0, N, 3)] = np.nan
+            P[rng.integers(0, N, 3)] = 0.0
+            P[rng.integers(0, N, 5)] = P[0]
+        lay = ["NMC", "MNC"][int(rng.integers(0, 2))]
+        host = P if lay == "NMC" else np.ascontiguousarray(np.transpose(P, (1, 0, 2)))
+        _, idx = ce.ops.select_mc(dev(host), q, lay)
+        exp = O.oracle_select_mc(P, q, "NMC")[1]
+        assert np.array_equal(idx_np(idx), exp), (case, N, M, C, q, dt, lay)
