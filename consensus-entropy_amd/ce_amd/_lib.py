@@ -34,6 +34,8 @@ SIGNATURES = {
     "ce_committee_entropy": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
     "ce_vote_entropy": (_int, [_vp, _i64, _i32, _i32, _i64, _vp, _vp, _vp]),
     "ce_va_entropy": (_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "ce_gnb_predict_proba": (_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
+    "ce_sgd_predict_proba": (_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "ce_segment_mean": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _vp, _i64, _vp, _int, _i64, _vp]),
     "ce_topq_workspace_bytes": (_sz, [_i64, _i32]),
     "ce_topq": (_int, [_vp, _i64, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),

@@ -139,6 +139,57 @@ def segment_mean(frames, offsets, perm=None, out=None):
     return out
 
 
+def _f64_dev(t, device, what):
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(t)
+    t = t.to(device=device, dtype=torch.float64)
+    return t.contiguous()
+
+
+def gnb_predict_proba(X, theta, var, class_prior, out=None):
+    """GaussianNB(...).predict_proba(X) on the device (sklearn 0.24.1 math,
+    deam_classifier.py:211; amg_test.py:435).  X [F, D] f64 frames; theta /
+    var [C, D] (theta_, var_ -- sigma_ in 0.24), class_prior [C]."""
+    _on_gpu(X, "X")
+    if X.dim() != 2 or X.dtype != torch.float64 or X.stride(1) != 1:
+        raise ValueError("X must be a float64 [F, D] tensor with unit column stride")
+    F, D = X.shape
+    theta = _f64_dev(theta, X.device, "theta")
+    var = _f64_dev(var, X.device, "var")
+    C = theta.shape[0]
+    if tuple(theta.shape) != (C, D) or tuple(var.shape) != (C, D):
+        raise ValueError(f"theta/var must be [C, {D}]")
+    log_prior = torch.log(_f64_dev(class_prior, X.device, "class_prior"))  # np.log(class_prior_[i])
+    if out is None:
+        out = torch.empty((F, C), dtype=torch.float64, device=X.device)
+    call("ce_gnb_predict_proba", _p(X), F, D, X.stride(0), _p(theta), _p(var), _p(log_prior), C, _p(out),
+         out.stride(0), _stream(X.device))
+    return out
+
+
+def sgd_predict_proba(X, coef, intercept, out=None):
+    """SGDClassifier(loss='log').predict_proba(X) on the device (sklearn
+    _predict_proba_lr, deam_classifier.py:214; amg_test.py:435).  coef [K, D],
+    intercept [K]; K = C (OvR) or 1 (binary, C = 2)."""
+    _on_gpu(X, "X")
+    if X.dim() != 2 or X.dtype != torch.float64 or X.stride(1) != 1:
+        raise ValueError("X must be a float64 [F, D] tensor with unit column stride")
+    F, D = X.shape
+    coef = _f64_dev(coef, X.device, "coef")
+    if coef.dim() == 1:
+        coef = coef.unsqueeze(0)
+    K = coef.shape[0]
+    intercept = _f64_dev(intercept, X.device, "intercept").reshape(-1)
+    C = 2 if K == 1 else K
+    if coef.shape[1] != D or intercept.numel() != K:
+        raise ValueError(f"coef must be [K, {D}] and intercept [K]")
+    if out is None:
+        out = torch.empty((F, C), dtype=torch.float64, device=X.device)
+    call("ce_sgd_predict_proba", _p(X), F, D, X.stride(0), _p(coef), _p(intercept), K, C, _p(out),
+         out.stride(0), _stream(X.device))
+    return out
+
+
 def _check_q(q):
     q = int(q)
     if q < 1 or q > _lib.CE_MAX_Q:

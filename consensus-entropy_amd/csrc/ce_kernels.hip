@@ -25,6 +25,7 @@
 #include "ce_topq.hpp"
 #include "ce_wide.hpp"
 #include "ce_stream.hpp"
+#include "ce_members.hpp"
 
 namespace ce {
 
@@ -1241,6 +1242,50 @@ extern "C" int ce_mark_selected(uint32_t* excl, int64_t N, const int64_t* idx, i
     if (n == 0 || N == 0) return CE_OK;
     hipLaunchKernelGGL(k_mark, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, excl, N, idx, n, base_idx);
     return check_launch("ce_mark_selected");
+}
+
+// ---- committee member inference ---------------------------
+template <class F>
+static int with_nf(int D, F&& f) {
+    const int nf = (D + 63) / 64;
+#define CE_NF(N_) if (nf <= N_) { f(std::integral_constant<int, N_>()); return CE_OK; }
+    CE_NF(1) CE_NF(2) CE_NF(3) CE_NF(4) CE_NF(5) CE_NF(6) CE_NF(8)
+#undef CE_NF
+    return CE_EUNSUPPORTED;
+}
+
+static int member_grid(int64_t F) { return (int)std::min<int64_t>(cdiv(F, 4), 8192); }
+
+extern "C" int ce_gnb_predict_proba(const double* X, int64_t F, int32_t D, int64_t ld, const double* theta,
+                                    const double* var, const double* log_prior, int32_t C, double* out,
+                                    int64_t ld_out, ce_stream_t stream) {
+    if (F < 0 || D < 1 || D > kMaxFeat || ld < D || C < 1 || C > kMaxMemberC || ld_out < C)
+        return fail(CE_EINVAL, "bad GaussianNB shapes F=%lld D=%d C=%d", (long long)F, D, C);
+    if ((F > 0 && (!X || !out)) || !theta || !var || !log_prior) return fail(CE_EINVAL, "null pointer");
+    if (F == 0) return CE_OK;
+    GnbArgs a{X, F, D, ld, theta, var, log_prior, C, out, ld_out};
+    const PwPlan pl = pw_plan(D);
+    with_nf(D, [&](auto nf) {
+        hipLaunchKernelGGL((k_gnb_proba<decltype(nf)::value>), dim3(member_grid(F)), dim3(256), 0,
+                           (hipStream_t)stream, a, pl);
+    });
+    return check_launch("ce_gnb_predict_proba");
+}
+
+extern "C" int ce_sgd_predict_proba(const double* X, int64_t F, int32_t D, int64_t ld, const double* coef,
+                                    const double* intercept, int32_t K, int32_t C, double* out, int64_t ld_out,
+                                    ce_stream_t stream) {
+    if (F < 0 || D < 1 || D > kMaxFeat || ld < D || C < 2 || C > kMaxMemberC || ld_out < C ||
+        !(K == C || (K == 1 && C == 2)))
+        return fail(CE_EINVAL, "bad SGD shapes F=%lld D=%d K=%d C=%d", (long long)F, D, K, C);
+    if ((F > 0 && (!X || !out)) || !coef || !intercept) return fail(CE_EINVAL, "null pointer");
+    if (F == 0) return CE_OK;
+    SgdArgs a{X, F, D, ld, coef, intercept, K, C, out, ld_out};
+    with_nf(D, [&](auto nf) {
+        hipLaunchKernelGGL((k_sgd_proba<decltype(nf)::value>), dim3(member_grid(F)), dim3(256), 0,
+                           (hipStream_t)stream, a);
+    });
+    return check_launch("ce_sgd_predict_proba");
 }
 
 // ---- top-q of an entropy vector -------------------------------------------

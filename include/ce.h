@@ -105,6 +105,26 @@ int ce_segment_mean(const void *frames, ce_dtype dt, int64_t F, int32_t C, int64
                     ce_dtype out_dt, int64_t ld_out, ce_stream_t stream);
 
 /*
+ * Committee member inference on the device -- the
+ * predict_proba of the reference's linear members (amg_test.py:435, :467;
+ * deam_classifier.py:211-218) over frames X [F, D] f64 (row stride ld),
+ * written to out [F, C] f64 (row stride ld_out), e.g. the input of
+ * ce_segment_mean.  D <= 512 features (the reference: 260), C <= 8 classes.
+ *   ce_gnb_predict_proba  GaussianNB (sklearn 0.24.1): theta / var [C, D]
+ *                         (theta_, sigma_), log_prior [C] = log(class_prior_);
+ *                         numpy's pairwise sums over features, scipy's logsumexp
+ *   ce_sgd_predict_proba  SGDClassifier(loss='log'): coef [K, D], intercept [K];
+ *                         expit(X coef^T + b), OvR-normalised for K = C > 2,
+ *                         [1-p, p] for a binary model (K = 1, C = 2)
+ */
+int ce_gnb_predict_proba(const double *X, int64_t F, int32_t D, int64_t ld, const double *theta,
+                         const double *var, const double *log_prior, int32_t C, double *out,
+                         int64_t ld_out, ce_stream_t stream);
+int ce_sgd_predict_proba(const double *X, int64_t F, int32_t D, int64_t ld, const double *coef,
+                         const double *intercept, int32_t K, int32_t C, double *out, int64_t ld_out,
+                         ce_stream_t stream);
+
+/*
  * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]
  * (amg_test.py:445, :452, :480).  Positions are reported as base_idx + i.
  * val_out: [q] f64, idx_out: [q] int64.

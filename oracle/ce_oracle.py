@@ -114,6 +114,45 @@ def ref_group_mean(values, s_id):
     return out, keys
 
 
+def ref_gnb_predict_proba(X, theta, var, class_prior):
+    """GaussianNB.predict_proba as the reference's pinned sklearn 0.24.1 +
+    scipy 1.5.4 compute it (amg_test.py:435 on the 'classifier_gnb' member,
+    deam_classifier.py:211): _joint_log_likelihood (np.log of the prior,
+    -0.5 * np.sum(np.log(2 pi var)), -0.5 * np.sum((X - theta)**2 / var, 1)),
+    then predict_log_proba with scipy 1.5.4's logsumexp (amax, non-finite max
+    -> 0, exp, sum, log, + max), then np.exp.  (The installed scipy >= 1.14
+    rewrote logsumexp; tests pin this restatement to the installed sklearn
+    within a stated tolerance.)"""
+    X = np.asarray(X, np.float64)
+    jll = []
+    for i in range(len(class_prior)):
+        jointi = np.log(class_prior[i])
+        n_ij = -0.5 * np.sum(np.log(2.0 * np.pi * var[i, :]))
+        n_ij -= 0.5 * np.sum(((X - theta[i, :]) ** 2) / (var[i, :]), 1)
+        jll.append(jointi + n_ij)
+    jll = np.array(jll).T
+    a_max = np.amax(jll, axis=1, keepdims=True)
+    a_max[~np.isfinite(a_max)] = 0
+    s = np.sum(np.exp(jll - a_max), axis=1)
+    log_prob_x = np.log(s) + np.squeeze(a_max, axis=1)
+    return np.exp(jll - np.atleast_2d(log_prob_x).T)
+
+
+def ref_sgd_predict_proba(X, coef, intercept):
+    """SGDClassifier(loss='log').predict_proba (sklearn 0.24.1
+    _predict_proba_lr; deam_classifier.py:214): expit(X coef^T + intercept),
+    then OvR normalisation, or [1 - p, p] for a binary model (numpy @ for the
+    dot products -- BLAS order, as the reference)."""
+    from scipy.special import expit
+
+    d = np.asarray(X, np.float64) @ np.asarray(coef, np.float64).T + intercept
+    if d.shape[1] == 1:
+        p = expit(d[:, 0])
+        return np.vstack([1 - p, p]).T
+    p = expit(d)
+    return p / p.sum(axis=1).reshape((p.shape[0], -1))
+
+
 def ref_vote_table(votes, C=4):
     """amg_test.py:109-115 on an int8 vote matrix (-1 = missing): per row,
     Counter over classes, then ``np.round(v / num_anno, 3)``.  Pure-Python loop

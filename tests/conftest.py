@@ -26,3 +26,22 @@ def golden(name):
 @pytest.fixture
 def load_golden():
     return golden
+
+
+def fitted_members(seed=260, n_test=3000):
+    """A GaussianNB and an SGDClassifier(log loss) fitted on synthetic 260-feature
+    frames of 4 quadrant classes (the reference's member types, deam_classifier.py
+    :211-218), plus held-out frames."""
+    import numpy as np
+    from sklearn.linear_model import SGDClassifier
+    from sklearn.naive_bayes import GaussianNB
+
+    rng = np.random.default_rng(seed)
+    D, C = 260, 4
+    centers = rng.normal(0, 1, (C, D))
+    y = rng.integers(0, C, 4000)
+    X = centers[y] + rng.normal(0, 2.0, (4000, D))
+    gnb = GaussianNB().fit(X, y)
+    sgd = SGDClassifier(loss="log_loss", penalty="l2", random_state=1987, max_iter=20, tol=None).fit(X, y)
+    Xt = centers[rng.integers(0, C, n_test)] + rng.normal(0, 2.0, (n_test, D))
+    return gnb, sgd, Xt

@@ -536,3 +536,54 @@ def test_randomised_selection_fuzz(ce):
         _, idx = ce.ops.select_mc(dev(host), q, lay)
         exp = O.oracle_select_mc(P, q, "NMC")[1]
         assert np.array_equal(idx_np(idx), exp), (case, N, M, C, q, dt, lay)
+
+
+def test_member_inference_vs_restatement(ce):
+    """§8(f)4: GaussianNB / SGD(log) predict_proba on the device against the
+    restatement of the pinned sklearn 0.24.1 + scipy 1.5.4 math.  Tolerance
+    rtol 1e-10: GNB differs only by device vs glibc exp/log (ulps, amplified by
+    |jll| ~ 1e3 at most); SGD's dot products use a fixed wave order, the
+    reference BLAS's."""
+    from conftest import fitted_members
+    from oracle.ce_oracle import ref_gnb_predict_proba, ref_sgd_predict_proba
+
+    gnb, sgd, Xt = fitted_members(n_test=20_000)
+    Xd = dev(Xt)
+    got = ce.ops.gnb_predict_proba(Xd, gnb.theta_, gnb.var_, gnb.class_prior_).cpu().numpy()
+    np.testing.assert_allclose(got, ref_gnb_predict_proba(Xt, gnb.theta_, gnb.var_, gnb.class_prior_),
+                               rtol=1e-10, atol=1e-300)
+    got = ce.ops.sgd_predict_proba(Xd, sgd.coef_, sgd.intercept_).cpu().numpy()
+    np.testing.assert_allclose(got, ref_sgd_predict_proba(Xt, sgd.coef_, sgd.intercept_), rtol=1e-10, atol=1e-300)
+    # a binary SGD model: [1 - p, p]
+    got = ce.ops.sgd_predict_proba(Xd, sgd.coef_[:1], sgd.intercept_[:1]).cpu().numpy()
+    np.testing.assert_allclose(got, ref_sgd_predict_proba(Xt, sgd.coef_[:1], sgd.intercept_[:1]), rtol=1e-10)
+
+
+def test_frames_inference_to_selection(ce):
+    """amg_test.py:426-445 with every step on the device: member inference over
+    frames (GNB, SGD), per-song segment mean, stack with a song-level member,
+    selection.  The selection equals the oracle's on the device's member
+    probabilities (the exact part of the path); the members themselves are
+    checked to tolerance above."""
+    from conftest import fitted_members
+    from oracle import ce_oracle as O
+    from oracle.ce_oracle import ref_group_mean
+
+    gnb, sgd, Xt = fitted_members(n_test=16_080)
+    s_id = np.repeat(np.arange(1608) * 5, 10)
+    Xd = dev(Xt)
+    fr_gnb = ce.ops.gnb_predict_proba(Xd, gnb.theta_, gnb.var_, gnb.class_prior_)
+    fr_sgd = ce.ops.sgd_predict_proba(Xd, sgd.coef_, sgd.intercept_)
+    uniq, offsets, perm = ce.song_groups(s_id)
+    assert perm is None
+    rng = np.random.default_rng(5)
+    cnn = rng.random((1608, 4)).astype(np.float32)
+    stack = torch.empty((3, 1608, 4), dtype=torch.float64, device="cuda")
+    ce.ops.segment_mean(fr_gnb, dev(offsets), out=stack[0])
+    ce.ops.segment_mean(fr_sgd, dev(offsets), out=stack[1])
+    stack[2] = dev(cnn).double()
+    _, idx = ce.ops.select_mc(stack, 10, "MNC")
+    P = np.array([ref_group_mean(fr_gnb.cpu().numpy(), s_id)[0], ref_group_mean(fr_sgd.cpu().numpy(), s_id)[0],
+                  cnn])
+    assert np.array_equal(stack.cpu().numpy(), P)
+    assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, 10, "MNC")[1])

@@ -166,3 +166,18 @@ def test_group_mean_restatement_vs_pandas():
         assert np.array_equal(keys, exp.index.values)
         assert got.dtype == exp.values.dtype
         assert np.array_equal(got, exp.values, equal_nan=True)
+
+
+def test_member_restatements_vs_sklearn():
+    """The restated predict_proba of the GaussianNB and SGD(log) members
+    against the installed sklearn on fitted models.  The restatement uses the
+    pinned scipy 1.5.4 logsumexp; the installed scipy's rewritten one and
+    BLAS's dot order differ by rounding only: rtol 1e-9 (stated)."""
+    from conftest import fitted_members
+    from oracle.ce_oracle import ref_gnb_predict_proba, ref_sgd_predict_proba
+
+    gnb, sgd, Xt = fitted_members()
+    p = ref_gnb_predict_proba(Xt, gnb.theta_, gnb.var_, gnb.class_prior_)
+    np.testing.assert_allclose(p, gnb.predict_proba(Xt), rtol=1e-9, atol=1e-300)
+    p = ref_sgd_predict_proba(Xt, sgd.coef_, sgd.intercept_)
+    np.testing.assert_allclose(p, sgd.predict_proba(Xt), rtol=1e-9, atol=1e-300)

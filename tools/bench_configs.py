@@ -138,7 +138,7 @@ def cpu_reference(only, reps=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="0,1,2,4,5")
+    ap.add_argument("--only", default="0,1,2,4,5,6")
     ap.add_argument("--cpu", action="store_true", help="also time the reference expressions on the host")
     args = ap.parse_args()
     only = {int(x) for x in args.only.split(",")}
@@ -193,6 +193,21 @@ def main():
         torch.cuda.empty_cache()
     if 5 in only:
         segment_mean_configs(g, report)
+    if 6 in only:  # §8(f)4: member inference over 260-feature frames (GNB, SGD log), C = 4
+        D, C = 260, 4
+        theta = torch.randn((C, D), device="cuda", dtype=torch.float64, generator=g)
+        var = torch.rand((C, D), device="cuda", dtype=torch.float64, generator=g) + 0.5
+        prior = torch.full((C,), 0.25, device="cuda", dtype=torch.float64)
+        coef = torch.randn((C, D), device="cuda", dtype=torch.float64, generator=g) * 0.05
+        icpt = torch.zeros(C, device="cuda", dtype=torch.float64)
+        for F in (64_320, 4_000_000):
+            X = torch.randn((F, D), device="cuda", dtype=torch.float64, generator=g)
+            reps = 200 if F < 100_000 else 20
+            t = timed(lambda: ops.gnb_predict_proba(X, theta, var, prior), reps)
+            report(f"(f)4 GaussianNB predict_proba {F} frames x {D} f64", F, F * D * 8, t)
+            t = timed(lambda: ops.sgd_predict_proba(X, coef, icpt), reps)
+            report(f"(f)4 SGD(log) predict_proba {F} frames x {D} f64", F, F * D * 8, t)
+            del X
 
 
 def segment_mean_configs(g, report_fn):
