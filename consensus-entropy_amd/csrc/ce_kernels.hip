@@ -1245,16 +1245,18 @@ extern "C" int ce_mark_selected(uint32_t* excl, int64_t N, const int64_t* idx, i
 }
 
 // ---- committee member inference ---------------------------
+// features per lane of the 8-lanes-per-frame kernels: ceil(D / 8), rounded up to a multiple of 8
 template <class F>
-static int with_nf(int D, F&& f) {
-    const int nf = (D + 63) / 64;
-#define CE_NF(N_) if (nf <= N_) { f(std::integral_constant<int, N_>()); return CE_OK; }
-    CE_NF(1) CE_NF(2) CE_NF(3) CE_NF(4) CE_NF(5) CE_NF(6) CE_NF(8)
-#undef CE_NF
+static int with_nx(int D, F&& f) {
+    const int nx = (D + 7) / 8;
+#define CE_NX(N_) if (nx <= N_) { f(std::integral_constant<int, N_>()); return CE_OK; }
+    CE_NX(8) CE_NX(16) CE_NX(24) CE_NX(32) CE_NX(36) CE_NX(40) CE_NX(48) CE_NX(56) CE_NX(64)
+#undef CE_NX
     return CE_EUNSUPPORTED;
 }
 
-static int member_grid(int64_t F) { return (int)std::min<int64_t>(cdiv(F, 4), 8192); }
+// >= ~8 eight-frame passes per wave, so each block's LDS staging is amortised
+static int member_grid8(int64_t F) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(F, 256), 2048)); }
 
 extern "C" int ce_gnb_predict_proba(const double* X, int64_t F, int32_t D, int64_t ld, const double* theta,
                                     const double* var, const double* log_prior, int32_t C, double* out,
@@ -1265,8 +1267,9 @@ extern "C" int ce_gnb_predict_proba(const double* X, int64_t F, int32_t D, int64
     if (F == 0) return CE_OK;
     GnbArgs a{X, F, D, ld, theta, var, log_prior, C, out, ld_out};
     const PwPlan pl = pw_plan(D);
-    with_nf(D, [&](auto nf) {
-        hipLaunchKernelGGL((k_gnb_proba<decltype(nf)::value>), dim3(member_grid(F)), dim3(256), 0,
+    const size_t lds = (size_t)2 * C * D * sizeof(double);
+    with_nx(D, [&](auto nx) {
+        hipLaunchKernelGGL((k_gnb_proba8<decltype(nx)::value>), dim3(member_grid8(F)), dim3(256), lds,
                            (hipStream_t)stream, a, pl);
     });
     return check_launch("ce_gnb_predict_proba");
@@ -1281,8 +1284,9 @@ extern "C" int ce_sgd_predict_proba(const double* X, int64_t F, int32_t D, int64
     if ((F > 0 && (!X || !out)) || !coef || !intercept) return fail(CE_EINVAL, "null pointer");
     if (F == 0) return CE_OK;
     SgdArgs a{X, F, D, ld, coef, intercept, K, C, out, ld_out};
-    with_nf(D, [&](auto nf) {
-        hipLaunchKernelGGL((k_sgd_proba<decltype(nf)::value>), dim3(member_grid(F)), dim3(256), 0,
+    const size_t lds = (size_t)K * D * sizeof(double);
+    with_nx(D, [&](auto nx) {
+        hipLaunchKernelGGL((k_sgd_proba8<decltype(nx)::value>), dim3(member_grid8(F)), dim3(256), lds,
                            (hipStream_t)stream, a);
     });
     return check_launch("ce_sgd_predict_proba");

@@ -16,7 +16,11 @@
 //     reference (an unspecified order); here a fixed wave-reduction order --
 //     parity is to a tolerance (tests state it).
 //
-// One wave per frame: lane l owns features l, l + 64, ... (coalesced row loads).
+// Eight lanes per frame, eight frames per wave: lane j of a group owns the
+// features f = 8m + j -- exactly numpy's eight pairwise accumulators (leaves
+// start at multiples of 8), so a leaf's sum is lane j's sequential chain
+// followed by the ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) butterfly of the group.
+// theta / var / coef are staged once per block in LDS.
 #pragma once
 #include "ce_device.hpp"
 #include "ce_stream.hpp"
@@ -40,67 +44,6 @@ struct GnbArgs {
     int64_t ldo;
 };
 
-// sum over the wave's LDS row a[0..D) in numpy's pairwise order
-__device__ __forceinline__ double row_pairwise(double* row, const PwPlan& pl) {
-    __builtin_amdgcn_wave_barrier();
-    const double s = wave_row_sum(row, pl, nullptr);
-    __builtin_amdgcn_wave_barrier();
-    return s;
-}
-
-template <int NF>  // features per lane (D <= 64 * NF)
-__global__ __launch_bounds__(256) void k_gnb_proba(GnbArgs a, PwPlan pl) {
-    __shared__ __attribute__((aligned(16))) double gsm[4 * kMaxFeat];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double* row = gsm + w * kMaxFeat;
-    // per class: -0.5 * np.sum(np.log(2. * np.pi * var_c)) (every wave computes it once)
-    double half_s1[kMaxMemberC];
-    for (int c = 0; c < a.C; ++c) {
-#pragma unroll
-        for (int k = 0; k < NF; ++k) {
-            const int f = lane + 64 * k;
-            if (f < a.D) row[f] = log(2. * M_PI * a.var[(int64_t)c * a.D + f]);
-        }
-        half_s1[c] = -0.5 * row_pairwise(row, pl);
-    }
-    for (int64_t fr = (int64_t)blockIdx.x * 4 + w; fr < a.F; fr += (int64_t)gridDim.x * 4) {
-        double x[NF];
-#pragma unroll
-        for (int k = 0; k < NF; ++k) {
-            const int f = lane + 64 * k;
-            x[k] = f < a.D ? a.X[fr * a.ld + f] : 0.0;
-        }
-        double jll[kMaxMemberC];
-        for (int c = 0; c < a.C; ++c) {
-#pragma unroll
-            for (int k = 0; k < NF; ++k) {
-                const int f = lane + 64 * k;
-                if (f < a.D) {
-                    const double d = x[k] - a.theta[(int64_t)c * a.D + f];
-                    row[f] = (d * d) / a.var[(int64_t)c * a.D + f];
-                }
-            }
-            const double s2 = row_pairwise(row, pl);
-            double n_ij = half_s1[c];
-            n_ij -= 0.5 * s2;
-            jll[c] = a.log_prior[c] + n_ij;
-        }
-        // scipy.special.logsumexp(jll, axis=1): max (non-finite -> 0), exp, sequential sum (C < 8), log
-        double mx = jll[0];
-        for (int c = 1; c < a.C; ++c) mx = jll[c] > mx ? jll[c] : mx;  // np.amax (NaN aside)
-        if (!__builtin_isfinite(mx)) mx = 0.0;
-        double s = -0.0;
-        for (int c = 0; c < a.C; ++c) s += exp(jll[c] - mx);
-        const double lse = log(0.0 + s) + mx;
-        if (lane < a.C) {
-            double v = 0.0;
-            for (int c = 0; c < a.C; ++c)
-                if (c == lane) v = exp(jll[c] - lse);
-            a.out[fr * a.ldo + lane] = v;
-        }
-    }
-}
-
 struct SgdArgs {
     const double* X;
     int64_t F;
@@ -113,30 +56,135 @@ struct SgdArgs {
     int64_t ldo;
 };
 
-template <int NF>
-__global__ __launch_bounds__(256) void k_sgd_proba(SgdArgs a) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int64_t fr = (int64_t)blockIdx.x * 4 + w; fr < a.F; fr += (int64_t)gridDim.x * 4) {
-        double x[NF];
+// np.sum of the terms t[m] (feature f = 8m + j of this lane's group; 0 past
+// D) in numpy's pairwise order; the result in every lane of the 8-lane group.
+// The terms are computed once by the caller; the leaf bounds are wave-uniform.
+template <int NX>
+__device__ __forceinline__ double group_pairwise(const double (&t)[NX], const PwPlan& pl) {
+    const int lane = threadIdx.x & 63, j = lane & 7, gb = lane & ~7;
+    double lv = 0.0;  // lane gb + l: leaf l's sum
+    for (int l = 0; l < pl.nleaves; ++l) {
+        const int st = pl.lstart[l], len = pl.llen[l];
+        const int nb = len - (len % 8);
+        const int m0 = st >> 3, m1 = (st + nb) >> 3;
+        double r = 0.0, tl = 0.0;
 #pragma unroll
-        for (int k = 0; k < NF; ++k) {
-            const int f = lane + 64 * k;
-            x[k] = f < a.D ? a.X[fr * a.ld + f] : 0.0;
+        for (int m = 0; m < NX; ++m) {
+            if (m == m0) r = t[m];
+            else if (m > m0 && m < m1) r += t[m];
+            if (m == m1) tl = t[m];  // tail elements st + nb + k sit in lanes gb + k of column m1
+        }
+        r = r + __shfl_xor(r, 1);
+        r = r + __shfl_xor(r, 2);
+        r = r + __shfl_xor(r, 4);
+        for (int k = 0; k < len % 8; ++k) r += __shfl(tl, gb + k);
+        if (j == l) lv = r;
+    }
+    for (int rd = 0; rd < pl.nrounds; ++rd) {
+        const int p = j < kPwMaxLeaves ? pl.partner[rd][j] : -1;
+        const double v = __shfl(lv, gb + (p >= 0 ? p : j));
+        if (p >= 0) lv = lv + v;
+    }
+    return 0.0 + __shfl(lv, gb);
+}
+
+// GaussianNB, 8 lanes per frame.  LDS: theta, var [C][D] doubles, and the
+// per-class -0.5 * np.sum(np.log(2 pi var_c)) (group c computes class c once).
+template <int NX>
+__global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
+    extern __shared__ __attribute__((aligned(16))) double msm[];
+    __shared__ double hs1[kMaxMemberC];
+    double* th = msm;
+    double* vr = msm + (int64_t)a.C * a.D;
+    for (int t = threadIdx.x; t < a.C * a.D; t += blockDim.x) {
+        th[t] = a.theta[t];
+        vr[t] = a.var[t];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 7, g = lane >> 3, w = threadIdx.x >> 6;
+    if (w * 8 < a.C) {  // wave-uniform: the waves holding groups 0..C-1
+        const int gid = w * 8 + g, c = gid < a.C ? gid : 0;
+        double t[NX];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) {
+            const int f = 8 * m + j;
+            t[m] = f < a.D ? log(2. * M_PI * vr[c * a.D + f]) : 0.0;
+        }
+        const double s1 = group_pairwise<NX>(t, pl);
+        if (gid < a.C && j == 0) hs1[gid] = -0.5 * s1;
+    }
+    __syncthreads();
+    const int64_t step = (int64_t)gridDim.x * 32;
+    for (int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 8; f0 < a.F; f0 += step) {
+        const int64_t fr = f0 + g;
+        const int64_t frc = fr < a.F ? fr : a.F - 1;  // clamped: every group loads
+        double x[NX];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) {
+            const int f = 8 * m + j;
+            x[m] = f < a.D ? a.X[frc * a.ld + f] : 0.0;
+        }
+        double jll[kMaxMemberC];
+        for (int c = 0; c < a.C; ++c) {
+            double t[NX];
+#pragma unroll
+            for (int m = 0; m < NX; ++m) {
+                const int f = 8 * m + j, fc = f < a.D ? f : 0;
+                const double d = x[m] - th[c * a.D + fc];
+                t[m] = f < a.D ? (d * d) / vr[c * a.D + fc] : 0.0;
+            }
+            const double s2 = group_pairwise<NX>(t, pl);
+            double n_ij = hs1[c];
+            n_ij -= 0.5 * s2;
+            jll[c] = a.log_prior[c] + n_ij;
+        }
+        double mx = jll[0];
+        for (int c = 1; c < a.C; ++c) mx = jll[c] > mx ? jll[c] : mx;
+        if (!__builtin_isfinite(mx)) mx = 0.0;
+        double s = -0.0;
+        for (int c = 0; c < a.C; ++c) s += exp(jll[c] - mx);
+        const double lse = log(0.0 + s) + mx;
+        if (fr < a.F && j < a.C) {
+            double v = 0.0;
+            for (int c = 0; c < a.C; ++c)
+                if (c == j) v = exp(jll[c] - lse);
+            a.out[fr * a.ldo + j] = v;
+        }
+    }
+}
+
+// SGDClassifier(loss='log'), 8 lanes per frame; coef in LDS.
+template <int NX>
+__global__ __launch_bounds__(256) void k_sgd_proba8(SgdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double msm[];
+    for (int t = threadIdx.x; t < a.K * a.D; t += blockDim.x) msm[t] = a.coef[t];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 7, g = lane >> 3, w = threadIdx.x >> 6;
+    const int64_t step = (int64_t)gridDim.x * 32;
+    for (int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 8; f0 < a.F; f0 += step) {
+        const int64_t fr = f0 + g;
+        const int64_t frc = fr < a.F ? fr : a.F - 1;
+        double x[NX];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) {
+            const int f = 8 * m + j;
+            x[m] = f < a.D ? a.X[frc * a.ld + f] : 0.0;
         }
         double p[kMaxMemberC];
         for (int c = 0; c < a.K; ++c) {
             double d = 0.0;
 #pragma unroll
-            for (int k = 0; k < NF; ++k) {
-                const int f = lane + 64 * k;
-                if (f < a.D) d = fma(x[k], a.coef[(int64_t)c * a.D + f], d);
+            for (int m = 0; m < NX; ++m) {
+                const int f = 8 * m + j;
+                if (f < a.D) d = fma(x[m], msm[c * a.D + f], d);
             }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
+            d = d + __shfl_xor(d, 1);
+            d = d + __shfl_xor(d, 2);
+            d = d + __shfl_xor(d, 4);
             d += a.intercept[c];
             p[c] = 1.0 / (1.0 + exp(-d));  // scipy.special.expit
         }
-        if (a.K == 1) {  // binary: np.vstack([1 - prob, prob]).T
+        if (a.K == 1) {
             p[1] = p[0];
             p[0] = 1.0 - p[1];
         } else {
@@ -145,13 +193,14 @@ __global__ __launch_bounds__(256) void k_sgd_proba(SgdArgs a) {
             s = 0.0 + s;
             for (int c = 0; c < a.K; ++c) p[c] /= s;
         }
-        if (lane < a.C) {
+        if (fr < a.F && j < a.C) {
             double v = 0.0;
             for (int c = 0; c < a.C; ++c)
-                if (c == lane) v = p[c];
-            a.out[fr * a.ldo + lane] = v;
+                if (c == j) v = p[c];
+            a.out[fr * a.ldo + j] = v;
         }
     }
 }
 
 }  // namespace ce
+
