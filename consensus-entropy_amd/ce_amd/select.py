@@ -92,24 +92,32 @@ def committee_from_frames(members, s_id, device=None):
     uniq, offsets, perm = song_groups(s_id)
     N = len(uniq)
     F = len(np.asarray(getattr(s_id, "values", s_id)))
-    arrs = [np.asarray(getattr(m, "values", m)) for m in members]
+    # members: device tensors (e.g. ops.gnb_predict_proba outputs) stay on the device
+    arrs = [m if isinstance(m, torch.Tensor) else np.asarray(getattr(m, "values", m)) for m in members]
     if not arrs:
         raise ValueError("committee has no members")
     C = arrs[0].shape[1]
-    dts = {a.dtype for a in arrs}
-    dt = torch.float32 if dts == {np.dtype(np.float32)} else torch.float64
+    f32 = [a.dtype in (np.float32, torch.float32) for a in arrs]
+    dt = torch.float32 if all(f32) else torch.float64
     stack = torch.empty((len(arrs), N, C), dtype=dt, device=dev)
     offs_d = torch.from_numpy(offsets).to(dev)
     perm_d = torch.from_numpy(perm).to(dev) if perm is not None else None
     for m, a in enumerate(arrs):
         if a.ndim != 2 or a.shape[1] != C:
-            raise ValueError(f"member {m} has shape {a.shape}, expected [*, {C}]")
+            raise ValueError(f"member {m} has shape {tuple(a.shape)}, expected [*, {C}]")
+        if isinstance(a, torch.Tensor):
+            t = a.to(dev)
+            if t.dtype not in (torch.float32, torch.float64):
+                t = t.to(torch.float64)
+        else:
+            t = None
         if a.shape[0] == F and (F != N or perm is not None):  # frame-level: groupby mean on the device
-            fr = torch.from_numpy(np.ascontiguousarray(a, dtype=a.dtype if a.dtype in (np.float32, np.float64)
-                                                       else np.float64)).to(dev)
-            ops.segment_mean(fr, offs_d, perm_d, out=stack[m])
+            if t is None:
+                t = torch.from_numpy(np.ascontiguousarray(a, dtype=a.dtype if a.dtype in (np.float32, np.float64)
+                                                          else np.float64)).to(dev)
+            ops.segment_mean(t.contiguous(), offs_d, perm_d, out=stack[m])
         elif a.shape[0] == N:  # song-level member
-            stack[m] = torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+            stack[m] = (t if t is not None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)).to(dt)
         else:
             raise ValueError(f"member {m} has {a.shape[0]} rows: neither {F} frames nor {N} songs")
     return stack, uniq

@@ -1,0 +1,56 @@
+"""The RCCL exchange itself on one GPU: a world-size-1 "nccl" process group
+(RCCL on ROCm) runs sharded_select_mc_records / allgather_cands end to end --
+stage 1, stage 2 into ce_cand records, the RCCL all-gather, ce_merge_cands --
+and must equal the single-call selection.  (N > 1 ranks need N GPUs; their
+exchange logic is covered by tests/test_dist.py on gloo.)"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_rccl_record_exchange_world1():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import torch.distributed as dist
+
+    import ce_amd
+    from ce_amd import dist as cdist
+    from ce_amd import ops
+    from oracle import ce_oracle as O
+
+    ce_amd.load()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(4)
+        e = -np.log(rng.random((200_003, 16, 4)))
+        P = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+        Pd = torch.from_numpy(P).cuda()
+        plan = ops.MCPlan(Pd, 10, "NMC")
+        plan.partial()
+        rec = plan.finish_cands()
+        recv = cdist.allgather_cands(rec)
+        assert torch.equal(recv, rec)
+        vals, idx = ops.merge_cands(recv, 10)
+        exp = O.oracle_select_mc(P, 10, "NMC")[1]
+        assert np.array_equal(idx.cpu().numpy(), exp)
+        # the packed (entropy, position) exchange too
+        v2, i2 = plan.finish()
+        av, ai = cdist.allgather_topq(v2, i2, 10)
+        v3, i3 = ops.topq_merge(av, ai, 10)
+        assert np.array_equal(i3.cpu().numpy(), exp)
+    finally:
+        dist.destroy_process_group()
