@@ -1549,7 +1549,7 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
             using S = decltype(src);
             with_seg_batching<S>([&](auto unr, auto ipl) {
                 hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>),
-                                   dim3((unsigned)nl), dim3(bpu == 1 ? 64 * kSegWaves : 256), 0, st, src, offsets,
+                                   dim3((unsigned)nl), dim3(bpu == 1 && U < 64 ? 64 * kSegWaves : 256), 0, st, src, offsets,
                                    (int64_t)0, (int64_t)0, q, bpu, val_out, idx_out, w.c, (const uint32_t*)nullptr);
             });
         });

@@ -561,3 +561,4 @@ __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_
 }
 
 }  // namespace ce
+
