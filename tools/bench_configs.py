@@ -132,8 +132,35 @@ def cpu_reference(only, reps=5):
         members = [dir_((n, 1000), np.float32) for _ in range(32)]
         t = med(lambda: mc(members), reps=3)
         out["configs[4] wide 32x1000 (per item)"] = t / n
+    if 5 in only:  # amg_test.py:437 groupby mean of one member, 1608 songs x 40 frames and 1M songs x 40 frames
+        for songs in (1608, 1_000_000):
+            F = songs * 40
+            s_id = np.repeat(np.arange(songs), 40)
+            vals = rng.random((F, 4))
+            out[f"(f) segment mean {songs} songs x 40 frames (pandas groupby)"] = med(
+                lambda: pd.DataFrame(vals, index=pd.Index(s_id, name="s_id")).groupby(["s_id"]).mean(), reps=3)
+    if 6 in only:  # deam_classifier.py:211-218 members' predict_proba on 64,320 frames x 260 features
+        from sklearn.linear_model import SGDClassifier
+        from sklearn.naive_bayes import GaussianNB
+
+        Xf = rng.normal(0, 1, (4000, 260))
+        yf = rng.integers(0, 4, 4000)
+        gnb = GaussianNB().fit(Xf, yf)
+        sgd = SGDClassifier(loss="log_loss", max_iter=5, tol=None).fit(Xf, yf)
+        X = rng.normal(0, 1, (64_320, 260))
+        out["(f)4 GaussianNB predict_proba 64320 frames (sklearn)"] = med(lambda: gnb.predict_proba(X), reps=3)
+        out["(f)4 SGD(log) predict_proba 64320 frames (sklearn)"] = med(lambda: sgd.predict_proba(X), reps=3)
     for k, v in out.items():
         print(json.dumps({"cpu_reference": k, "s": v, "threads": 1}), flush=True)
+
+
+def cpu_reference_1thread(only):
+    """cpu_reference with BLAS / OpenMP pools limited to one thread (the box
+    exports OMP_NUM_THREADS=16; the sklearn members' predict_proba uses BLAS)."""
+    from threadpoolctl import threadpool_limits
+
+    with threadpool_limits(limits=1):
+        cpu_reference(only)
 
 
 def main():
@@ -143,7 +170,7 @@ def main():
     args = ap.parse_args()
     only = {int(x) for x in args.only.split(",")}
     if args.cpu:
-        cpu_reference(only)
+        cpu_reference_1thread(only)
     g = torch.Generator(device="cuda").manual_seed(1987)
     q = 10
     if 0 in only:  # configs[0]: 4-member committee x 1608 x 4, mixed f32/f64 -> f64 stack
