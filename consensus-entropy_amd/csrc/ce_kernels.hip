@@ -717,17 +717,26 @@ __global__ __launch_bounds__(kBS) void k_segment_mean(const void* __restrict__ f
         const int64_t f0 = offsets[n], f1 = offsets[n + 1];
         double sum = 0.0;
         int64_t cnt = 0;
-        for (int64_t f = f0; f < f1; ++f) {
-            const int64_t r = perm ? perm[f] : f;
-            double v;
-            if constexpr (DT == kF32)
-                v = (double)static_cast<const float*>(frames)[r * ld + c];
-            else
-                v = static_cast<const double*>(frames)[r * ld + c];
-            if (v == v) {  // not NaN
-                sum += v;
-                ++cnt;
+        // batches of 8 frames: the 8 loads are issued together (clamped rows,
+        // no branch around a load), then added in row order
+        constexpr int B = 8;
+        for (int64_t fb = f0; fb < f1; fb += B) {
+            double v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const int64_t f = fb + u < f1 ? fb + u : f1 - 1;
+                const int64_t r = perm ? perm[f] : f;
+                if constexpr (DT == kF32)
+                    v[u] = (double)static_cast<const float*>(frames)[r * ld + c];
+                else
+                    v[u] = static_cast<const double*>(frames)[r * ld + c];
             }
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (fb + u < f1 && v[u] == v[u]) {  // not NaN
+                    sum += v[u];
+                    ++cnt;
+                }
         }
         double m = cnt ? sum / (double)cnt : __longlong_as_double(0x7ff8000000000000ll);
         if constexpr (DT == kF32) m = (double)(float)m;  // the float32 result column
