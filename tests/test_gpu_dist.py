@@ -54,3 +54,31 @@ def test_rccl_record_exchange_world1():
         assert np.array_equal(i3.cpu().numpy(), exp)
     finally:
         dist.destroy_process_group()
+
+
+def test_bench_contract_small():
+    """bench.py's JSON line (the driver's contract) on a small pool: the
+    required keys, roofline / cpu_baseline objects, and a selection that
+    equals the oracle's on the same synthetic pool."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--n-items", "2000000", "--steps", "3",
+                        "--warmup", "1", "--cpu-sample", "200000"], capture_output=True, text=True, timeout=600,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["steps"] == 3 and line["value"] > 0
+    rf = line["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1.2
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] in ("port", "reference")
+    assert len(line["selected"]) == 10
