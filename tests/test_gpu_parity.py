@@ -587,3 +587,27 @@ def test_frames_inference_to_selection(ce):
                   cnn])
     assert np.array_equal(stack.cpu().numpy(), P)
     assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, 10, "MNC")[1])
+
+
+@pytest.mark.parametrize("dt,C,M", [("f32", 4, 16), ("f32", 4, 32), ("bf16", 4, 32), ("bf16", 4, 64), ("f64", 4, 16),
+                                    ("f32", 8, 8), ("f32", 8, 16)])
+def test_lds_dma_stream_instantiations(ce, dt, C, M):
+    """Every k_stream_nmc instantiation (item-major rows of 256 / 512 B staged
+    by LDS-DMA) against the oracle, with a ragged tail (N not a multiple of
+    64) and exact ties."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(M * 10 + C)
+    N = 100_003
+    P = synth(rng, N, M, C, np.float32, quant=32)
+    if dt == "bf16":
+        host = _bf16_bits(P)
+        Pd = dev(host.view(np.int16)).view(torch.bfloat16)
+    else:
+        host = P.astype(np.float64) if dt == "f64" else P
+        Pd = dev(host)
+    exp = O.oracle_select_mc(host, 10, "NMC")[1]
+    _, idx = ce.ops.select_mc(Pd, 10, "NMC")
+    assert np.array_equal(idx_np(idx), exp)
+    _, idx = ce.ops.select_mc(Pd, 64, "NMC")
+    assert np.array_equal(idx_np(idx), O.oracle_select_mc(host, 64, "NMC")[1])
