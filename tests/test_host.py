@@ -1,0 +1,68 @@
+"""Host logic that needs no GPU: the groupby geometry, the C-ABI's argument
+checks for the newer entry points, and the Python validation in front of them."""
+import ctypes
+
+import numpy as np
+import pytest
+
+
+def test_song_groups_matches_pandas_groupby():
+    import pandas as pd
+
+    from ce_amd import song_groups
+
+    rng = np.random.default_rng(3)
+    for grouped in (True, False):
+        s_id = rng.integers(0, 50, 2000) * 3 + 11
+        if grouped:
+            s_id = np.sort(s_id)
+        uniq, offsets, perm = song_groups(s_id)
+        exp = pd.Series(np.arange(len(s_id)), index=s_id).groupby(level=0)
+        assert np.array_equal(uniq, np.array(sorted(exp.groups)))
+        assert (perm is None) == grouped
+        order = np.arange(len(s_id)) if perm is None else perm
+        for g, key in enumerate(uniq):
+            rows = order[offsets[g]:offsets[g + 1]]
+            assert np.array_equal(rows, np.flatnonzero(s_id == key))  # row order kept (stable)
+    uniq, offsets, perm = song_groups(["b", "a", "b", "c"])
+    assert list(uniq) == ["a", "b", "c"] and offsets.tolist() == [0, 1, 3, 4] and perm.tolist() == [1, 0, 2, 3]
+
+
+def test_new_entry_points_validate_without_gpu():
+    from ce_amd import _lib
+
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)
+    assert lib.ce_excl_words(0) == 0 and lib.ce_excl_words(33) == 2
+    # q > 64 with an exclusion bitmap / candidate records: unsupported
+    rc = lib.ce_select_mc_excl(p, 0, 100, 4, 4, 16, 4, 1, p, 65, 0, p, 1 << 20, p, p, None)
+    assert rc == _lib.CE_EUNSUPPORTED
+    rc = lib.ce_select_finish_cands(100, 65, p, 1 << 20, p, None)
+    assert rc == _lib.CE_EUNSUPPORTED
+    rc = lib.ce_select_finish_cands(100, 10, p, 1 << 20, ctypes.c_void_p(24), None)  # misaligned records
+    assert rc == _lib.CE_EINVAL
+    rc = lib.ce_merge_cands(None, 8, 10, p, p, None)
+    assert rc == _lib.CE_EINVAL
+    # segment mean: bad dtype, bad strides
+    rc = lib.ce_segment_mean(p, 2, 10, 4, 4, None, p, 3, p, 1, 4, None)
+    assert rc == _lib.CE_EUNSUPPORTED
+    rc = lib.ce_segment_mean(p, 1, 10, 4, 3, None, p, 3, p, 1, 4, None)
+    assert rc == _lib.CE_EINVAL
+    # member inference: too many features / classes, inconsistent K
+    rc = lib.ce_gnb_predict_proba(p, 10, 513, 513, p, p, p, 4, p, 4, None)
+    assert rc == _lib.CE_EINVAL
+    rc = lib.ce_sgd_predict_proba(p, 10, 260, 260, p, p, 3, 4, p, 4, None)
+    assert rc == _lib.CE_EINVAL
+    assert lib.ce_mark_selected(None, 10, p, 1, 0, None) == _lib.CE_EINVAL
+
+
+def test_python_guards_without_gpu():
+    torch = pytest.importorskip("torch")
+    from ce_amd import ops
+
+    with pytest.raises(ValueError, match="HIP device"):
+        ops.segment_mean(torch.zeros((4, 4), dtype=torch.float64), torch.zeros(2, dtype=torch.int64))
+    with pytest.raises(ValueError, match="HIP device"):
+        ops.gnb_predict_proba(torch.zeros((4, 4), dtype=torch.float64), np.zeros((2, 4)), np.ones((2, 4)), [0.5, 0.5])
+    with pytest.raises(ValueError, match="HIP device"):
+        ops.merge_cands(torch.zeros((10, 2), dtype=torch.int64), 10)
