@@ -36,6 +36,10 @@ SIGNATURES = {
     "ce_va_entropy": (_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "ce_gnb_predict_proba": (_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "ce_sgd_predict_proba": (_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
+    "ce_xgb_predict_proba": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _vp, _vp, _i32, _i32, ctypes.c_float, _i32,
+                                    _vp, _int, _i64, _vp]),
+    "ce_xgb_lds_bytes": (_sz, [_i32, _i32]),
+    "ce_xgb_expf": (_int, [_vp, _i64, _vp, _vp]),
     "ce_segment_mean": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _vp, _i64, _vp, _int, _i64, _vp]),
     "ce_topq_workspace_bytes": (_sz, [_i64, _i32]),
     "ce_topq": (_int, [_vp, _i64, _i32, _i64, _vp, _sz, _vp, _vp, _vp]),

@@ -190,6 +190,34 @@ def sgd_predict_proba(X, coef, intercept, out=None):
     return out
 
 
+def xgb_predict_proba(X, forest, out=None, out_dtype=torch.float32):
+    """XGBClassifier(...).predict_proba(X) on the device (xgboost 1.3.3
+    predictor restated in csrc/ce_xgb.hip; xgboost/sklearn.py:991-1029,
+    amg_test.py:435).  X [F, D] f32/f64 frames (cast to float32 like DMatrix,
+    NaN = missing); ``forest`` an ``ce_amd.xgb.XgbForest`` (or its JSON).
+    Returns [F, C] ``out_dtype`` (float32 = what xgboost returns; float64 = its
+    exact upcast, ready for a committee stack)."""
+    from .xgb import XgbForest
+
+    _on_gpu(X, "X")
+    if X.dim() != 2 or X.dtype not in (torch.float32, torch.float64) or X.stride(1) != 1:
+        raise ValueError("X must be a float32/float64 [F, D] tensor with unit column stride")
+    if not isinstance(forest, XgbForest):
+        forest = XgbForest.from_json(forest)
+    F, D = X.shape
+    nodes, leaves, goff, depth = forest.device_arrays(X.device)
+    if forest.max_feature() >= D:
+        raise ValueError(f"the forest splits on feature {forest.max_feature()} but X has {D} columns")
+    G, C = forest.n_groups, forest.n_classes
+    if out is None:
+        out = torch.empty((F, C), dtype=out_dtype, device=X.device)
+    if out.dim() != 2 or out.shape[0] != F or out.shape[1] < C or out.stride(1) != 1 or out.dtype not in _DT:
+        raise ValueError(f"out must be a float [{F}, >={C}] tensor with unit column stride")
+    call("ce_xgb_predict_proba", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(nodes), _p(leaves), _p(goff), G, depth,
+         float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0), _stream(X.device))
+    return out
+
+
 def _check_q(q):
     q = int(q)
     if q < 1 or q > _lib.CE_MAX_Q:

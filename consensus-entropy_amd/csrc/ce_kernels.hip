@@ -26,6 +26,7 @@
 #include "ce_wide.hpp"
 #include "ce_stream.hpp"
 #include "ce_members.hpp"
+#include "ce_abi.hpp"
 
 namespace ce {
 
@@ -756,8 +757,7 @@ using namespace ce;
 
 static thread_local char g_err[512] = "";
 
-static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-static int fail(int code, const char* fmt, ...) {
+int fail(int code, const char* fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof g_err, fmt, ap);
@@ -765,7 +765,7 @@ static int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-static int check_launch(const char* what) {
+int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(CE_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     g_err[0] = 0;

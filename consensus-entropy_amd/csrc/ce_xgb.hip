@@ -1,0 +1,265 @@
+// ce_xgb.hip -- on-device XGBClassifier.predict_proba (the
+// 'classifier_xgb' committee member: amg_test.py:435 / :467 ->
+// xgboost/sklearn.py:991-1029 -> libxgboost 1.3.3, requirements.txt:50).
+//
+// What the reference computes (xgboost 1.3.3 CPU predictor, restated):
+//   * DMatrix(X): X (f64 DataFrame values) cast to float32 (round to nearest);
+//     NaN = missing (sklearn.py:1020, missing=np.nan);
+//   * per row, margins preds[g] start at the base margin (base_score for
+//     multi:softprob; ProbToMargin(base_score) = -logf(1/b - 1) for
+//     binary:logistic) and every tree, IN MODEL ORDER, adds its leaf to the
+//     margin of its group tree_info[t]: preds[g] += leaf (float32, sequential);
+//   * a tree is walked from the root: missing feature -> the default child,
+//     else fvalue < split_cond ? left : right (RegTree::GetNext);
+//   * multi:softprob: Softmax over the row (first maximum; e_c = expf(m_c - max);
+//     wsum += e_c in float32 from 0; e_c /= wsum); binary:logistic:
+//     p = 1 / (1 + expf(-m)), returned as [1 - p, p] (sklearn.py:1027-1029).
+//   * expf is glibc's (>= 2.27, the x86-64 FMA ifunc variant): restated below
+//     and verified bit-identical to the host's libm on all 2^32 floats
+//     (tests/test_oracle.py, tests/test_gpu_parity.py).
+//
+// Layout (packed on the host by ce_amd.xgb.XgbForest): every tree is padded to
+// a perfect binary tree of the forest's maximum depth d (an early leaf's
+// subtree repeats its value, so either branch below it reaches the same leaf);
+// internal node i has children 2i+1 / 2i+2.  Trees are stored group-major
+// (group g owns trees [goff[g], goff[g+1]), model order kept inside a group,
+// which is exactly the order the reference adds them to preds[g]).
+//   nodes  [T][2^d - 1] x {feature | default_left << 31, split_cond bits}
+//   leaves [T][2^d] f32
+//
+// Kernel: one block per 64-frame tile.  The tile's features are staged ONCE as
+// float32 in LDS, feature-major [D][65] (lane = frame: a wave's feature reads
+// hit 64 different rows of one column).  Wave w owns the groups g = w, w+4
+// (no cross-wave exchange: each group's margin is one lane-private float
+// chain, added in model order), walking 8 trees at a time so 8 independent
+// node-load -> LDS-read -> compare chains are in flight per lane.  Bound:
+// X bytes from HBM (D * sizeof(x) per frame) vs. T * d node steps per frame.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/ce.h"
+#include "ce_abi.hpp"
+
+namespace ce {
+
+constexpr int kXgbTile = 64;      // frames per block
+constexpr int kXgbPad = 65;       // LDS column stride (floats)
+constexpr int kXgbIlp = 8;        // trees walked together per wave
+constexpr int kXgbMaxDepth = 10;  // packed depth limit (2^10 leaves per tree)
+constexpr int kXgbMaxFeat = 512;
+constexpr int kXgbMaxGroups = 8;
+
+// glibc expf (sysdeps/ieee754/flt-32/e_expf.c, EXP2F_TABLE_BITS = 5), as the
+// x86-64 FMA ifunc variant evaluates it: tab[i] = bits(2^(i/32)) - (i << 52) / 32.
+__constant__ uint64_t kExp2fTab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+
+__device__ __forceinline__ float glibc_expf(float x) {
+    const uint32_t ux = __float_as_uint(x);
+    const uint32_t abstop = (ux >> 20) & 0x7ff;
+    if (abstop >= 0x42bu) {  // |x| >= 88 or NaN
+        if (ux == 0xff800000u) return 0.0f;
+        if (abstop >= 0x7f8u) return x + x;
+        if (x > 0x1.62e42ep6f) return __uint_as_float(0x7f800000u);
+        if (x < -0x1.9fe368p6f) return 0.0f;
+    }
+    constexpr double kN = 32.0;
+    const double inv_ln2_n = 0x1.71547652b82fep+0 * kN;
+    const double c0 = 0x1.c6af84b912394p-5 / kN / kN / kN, c1 = 0x1.ebfce50fac4f3p-3 / kN / kN,
+                 c2 = 0x1.62e42ff0c52d6p-1 / kN;
+    const double shift = 0x1.8p+52;
+    const double xd = (double)x;
+    const double z = inv_ln2_n * xd;
+    double kd = z + shift;
+    const uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd -= shift;
+    const double r = __builtin_fma(inv_ln2_n, xd, -kd);  // the FMA build contracts z - kd
+    uint64_t t = kExp2fTab[ki % 32];
+    t += ki << (52 - 5);
+    const double s = __longlong_as_double((long long)t);
+    const double zz = __builtin_fma(c0, r, c1);
+    const double r2 = r * r;
+    double y = __builtin_fma(c2, r, 1.0);
+    y = __builtin_fma(zz, r2, y);
+    y = y * s;
+    return (float)y;
+}
+
+struct XgbArgs {
+    const void* X;
+    int64_t F;
+    int D;
+    int64_t ld;
+    const uint2* nodes;   // [T][NI]
+    const float* leaves;  // [T][NI + 1]
+    const int32_t* goff;  // [G + 1]
+    int depth, NI, G, C;
+    float base;
+    void* out;
+    int64_t ldo;
+};
+
+template <int XDT, int ODT>
+__global__ __launch_bounds__(256) void k_xgb_proba(XgbArgs a) {
+    extern __shared__ float xsm[];
+    float* xs = xsm;                          // [D][kXgbPad]
+    float* mg = xsm + a.D * kXgbPad;          // [G][64] final margins
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int64_t f0 = (int64_t)blockIdx.x * kXgbTile;
+    const int nf = (int)min<int64_t>(kXgbTile, a.F - f0);
+
+    // ---- stage the tile: element e = (row r, feature f), 8 loads in flight ----
+    {
+        const int total = kXgbTile * a.D;
+        for (int e0 = threadIdx.x; e0 < total; e0 += blockDim.x * 8) {
+            float v[8];
+            int dst[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * blockDim.x;
+                const int ec = e < total ? e : total - 1;
+                const int r = ec / a.D, f = ec - r * a.D;
+                const int64_t row = f0 + (r < nf ? r : nf - 1);  // pad rows repeat the last frame
+                if constexpr (XDT == CE_F64)
+                    v[u] = (float)static_cast<const double*>(a.X)[row * a.ld + f];
+                else
+                    v[u] = static_cast<const float*>(a.X)[row * a.ld + f];
+                dst[u] = e < total ? f * kXgbPad + r : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (dst[u] >= 0) xs[dst[u]] = v[u];
+        }
+    }
+    __syncthreads();
+
+    // ---- wave w: groups w, w + nw, ...; 8 trees of a group walked together ----
+    const int NL = a.NI + 1;
+    for (int g = w; g < a.G; g += nw) {
+        const int k0 = a.goff[g], k1 = a.goff[g + 1];
+        float m = a.base;
+        for (int k = k0; k < k1; k += kXgbIlp) {
+            int idx[kXgbIlp];
+            const uint2* tn[kXgbIlp];
+#pragma unroll
+            for (int j = 0; j < kXgbIlp; ++j) {
+                const int kk = k + j < k1 ? k + j : k1 - 1;
+                tn[j] = a.nodes + (int64_t)kk * a.NI;
+                idx[j] = 0;
+            }
+            for (int lev = 0; lev < a.depth; ++lev) {
+                uint2 nd[kXgbIlp];
+#pragma unroll
+                for (int j = 0; j < kXgbIlp; ++j) nd[j] = tn[j][idx[j]];
+#pragma unroll
+                for (int j = 0; j < kXgbIlp; ++j) {
+                    const int ft = min((int)(nd[j].x & 0x7fffffffu), a.D - 1);  // packer checks < D; clamp keeps LDS in range
+                    const float x = xs[ft * kXgbPad + lane];
+                    // missing -> default child; else fvalue < split_cond ? left : right
+                    const bool right = __builtin_isnan(x) ? (nd[j].x >> 31) == 0u
+                                                         : !(x < __uint_as_float(nd[j].y));
+                    idx[j] = 2 * idx[j] + 1 + (right ? 1 : 0);
+                }
+            }
+            float lv[kXgbIlp];
+#pragma unroll
+            for (int j = 0; j < kXgbIlp; ++j) {
+                const int kk = k + j < k1 ? k + j : k1 - 1;
+                lv[j] = a.leaves[(int64_t)kk * NL + (idx[j] - a.NI)];
+            }
+#pragma unroll
+            for (int j = 0; j < kXgbIlp; ++j)
+                if (k + j < k1) m += lv[j];  // preds[g] += leaf, model order
+        }
+        mg[g * 64 + lane] = m;
+    }
+    __syncthreads();
+
+    // ---- transform (wave 0, one frame per lane) ----
+    if (w == 0 && lane < nf) {
+        const int64_t fr = f0 + lane;
+        float p[kXgbMaxGroups];
+        if (a.G == 1) {  // binary:logistic -> [1 - p, p]
+            const float m = mg[lane];
+            const float p1 = 1.0f / (1.0f + glibc_expf(-m));
+            p[0] = 1.0f - p1;
+            p[1] = p1;
+        } else {  // multi:softprob -> common::Softmax
+            float mx = mg[lane];
+            for (int g = 1; g < a.G; ++g) {
+                const float v = mg[g * 64 + lane];
+                if (v > mx) mx = v;
+            }
+            float wsum = 0.0f;
+            for (int g = 0; g < a.G; ++g) {
+                p[g] = glibc_expf(mg[g * 64 + lane] - mx);
+                wsum += p[g];
+            }
+            for (int g = 0; g < a.G; ++g) p[g] /= wsum;
+        }
+        for (int c = 0; c < a.C; ++c) {
+            if constexpr (ODT == CE_F64)
+                static_cast<double*>(a.out)[fr * a.ldo + c] = (double)p[c];
+            else
+                static_cast<float*>(a.out)[fr * a.ldo + c] = p[c];
+        }
+    }
+}
+
+__global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        y[i] = glibc_expf(x[i]);
+}
+
+}  // namespace ce
+
+using namespace ce;
+
+extern "C" size_t ce_xgb_lds_bytes(int32_t D, int32_t G) {
+    return (size_t)D * kXgbPad * sizeof(float) + (size_t)std::max(G, 1) * 64 * sizeof(float);
+}
+
+extern "C" int ce_xgb_predict_proba(const void* X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld,
+                                    const uint32_t* nodes, const float* leaves, const int32_t* group_offsets,
+                                    int32_t G, int32_t depth, float base_margin, int32_t C, void* out,
+                                    ce_dtype out_dt, int64_t ld_out, ce_stream_t stream) {
+    if (F < 0 || D < 1 || D > kXgbMaxFeat || ld < D || depth < 0 || depth > kXgbMaxDepth || G < 1 ||
+        G > kXgbMaxGroups || ld_out < C || !(G == C || (G == 1 && C == 2)))
+        return fail(CE_EINVAL, "bad XGB shapes F=%lld D=%d depth=%d G=%d C=%d", (long long)F, D, depth, G, C);
+    if ((x_dt != CE_F32 && x_dt != CE_F64) || (out_dt != CE_F32 && out_dt != CE_F64))
+        return fail(CE_EINVAL, "XGB dtypes must be F32 or F64");
+    if ((F > 0 && (!X || !out)) || !nodes || !leaves || !group_offsets) return fail(CE_EINVAL, "null pointer");
+    if (F == 0) return CE_OK;
+    XgbArgs a{X, F, D, ld, reinterpret_cast<const uint2*>(nodes), leaves, group_offsets,
+              depth, (1 << depth) - 1, G, C, base_margin, out, ld_out};
+    const size_t lds = ce_xgb_lds_bytes(D, G);
+    const int threads = 64 * std::min(G, 4);
+    const dim3 grid((unsigned)((F + kXgbTile - 1) / kXgbTile));
+    auto launch = [&](auto kern) {
+        if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, grid, dim3(threads), lds, (hipStream_t)stream, a);
+    };
+    if (x_dt == CE_F64)
+        out_dt == CE_F64 ? launch(k_xgb_proba<CE_F64, CE_F64>) : launch(k_xgb_proba<CE_F64, CE_F32>);
+    else
+        out_dt == CE_F64 ? launch(k_xgb_proba<CE_F32, CE_F64>) : launch(k_xgb_proba<CE_F32, CE_F32>);
+    return check_launch("ce_xgb_predict_proba");
+}
+
+extern "C" int ce_xgb_expf(const float* x, int64_t n, float* y, ce_stream_t stream) {
+    if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad expf arguments");
+    if (n == 0) return CE_OK;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_expf, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, n, y);
+    return check_launch("ce_xgb_expf");
+}

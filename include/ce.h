@@ -125,6 +125,32 @@ int ce_sgd_predict_proba(const double *X, int64_t F, int32_t D, int64_t ld, cons
                          ce_stream_t stream);
 
 /*
+ * XGBClassifier.predict_proba on the device (the
+ * 'classifier_xgb' member; amg_test.py:435/:467 -> xgboost/sklearn.py:991-1029
+ * -> libxgboost 1.3.3 CPU predictor, restated in csrc/ce_xgb.hip).
+ * X [F, D] (x_dt F32|F64, row stride ld; cast to float32 like DMatrix, NaN =
+ * missing), D <= 512.  The forest is packed by ce_amd.xgb.XgbForest: every tree
+ * padded to a perfect tree of depth `depth` (<= 10), stored group-major --
+ * group g owns trees [group_offsets[g], group_offsets[g+1]) in model order:
+ *   nodes  [T][2^depth - 1][2] u32 {feature | default_left << 31, split_cond bits}
+ *   leaves [T][2^depth] f32
+ * Every feature index must be < D.  G = C groups -> multi:softprob (softmax),
+ * G = 1 and C = 2 -> binary:logistic ([1 - p, p]); C <= 8.  base_margin is the
+ * margin every group starts from (base_score for softprob, -logf(1/b - 1) for
+ * logistic).  out [F, C] (out_dt F32 = what xgboost returns, F64 = its exact
+ * upcast, e.g. a committee stack), row stride ld_out.  Bit-identical to the
+ * restated predictor, including glibc's expf in the softmax.
+ *   ce_xgb_lds_bytes  dynamic LDS one block uses (host arithmetic)
+ *   ce_xgb_expf       the restated glibc expf over x [n] -> y [n] (verification)
+ */
+int ce_xgb_predict_proba(const void *X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld,
+                         const uint32_t *nodes, const float *leaves, const int32_t *group_offsets,
+                         int32_t G, int32_t depth, float base_margin, int32_t C, void *out,
+                         ce_dtype out_dt, int64_t ld_out, ce_stream_t stream);
+size_t ce_xgb_lds_bytes(int32_t D, int32_t G);
+int ce_xgb_expf(const float *x, int64_t n, float *y, ce_stream_t stream);
+
+/*
  * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]
  * (amg_test.py:445, :452, :480).  Positions are reported as base_idx + i.
  * val_out: [q] f64, idx_out: [q] int64.

@@ -250,3 +250,127 @@ int64_t ce_ref_topq_merge(const double *vals, const int64_t *idx, int64_t L, int
     }
     return k;
 }
+
+/* ---------------------------------------------------------------------------
+ * XGBClassifier.predict_proba (the 'classifier_xgb' member:
+ * amg_test.py:435/:467 -> xgboost/sklearn.py:991-1029 -> libxgboost 1.3.3,
+ * requirements.txt:50).  The C++ core is not in /root/reference and xgboost is
+ * not installed here: this restates its published CPU predictor (PARITY
+ * UNPINNED against xgboost itself; the engine is pinned to this restatement):
+ *   - DMatrix from the f64 array: values cast to float32; NaN = missing;
+ *   - preds[row][g] = base margin; for every tree t in MODEL order:
+ *     walk from node 0 -- missing -> default child, else
+ *     fvalue < split_cond ? left : right (RegTree::GetNext) -- until a leaf,
+ *     then preds[row][tree_info[t]] += leaf (float32)  (PredictByAllTrees);
+ *   - multi:softprob: common::Softmax (first max; expf(m - max); wsum float
+ *     from 0; divide); binary:logistic: 1/(1+expf(-m)) -> [1-p, p].
+ * The trees are the model's own node arrays (xgboost JSON: left_children,
+ * right_children, split_indices, split_conditions -- the leaf value at a leaf
+ * --, default_left), tree t's nodes at [node_off[t], node_off[t+1]).
+ * expf: glibc's algorithm (e_expf.c, 32-entry exp2 table) as the x86-64 FMA
+ * variant evaluates it; ce_ref_expf_mismatches compares it with libm's expf.
+ * ------------------------------------------------------------------------- */
+static const uint64_t kExp2fTab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+
+static uint32_t f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+float ce_ref_expf(float x) {
+    const uint32_t abstop = (f32_bits(x) >> 20) & 0x7ff;
+    if (abstop >= (f32_bits(88.0f) >> 20)) {
+        if (f32_bits(x) == f32_bits(-INFINITY)) return 0.0f;
+        if (abstop >= (f32_bits(INFINITY) >> 20)) return x + x;
+        if (x > 0x1.62e42ep6f) return INFINITY;
+        if (x < -0x1.9fe368p6f) return 0.0f;
+    }
+    const double N = 32.0, inv_ln2_n = 0x1.71547652b82fep+0 * N;
+    const double c0 = 0x1.c6af84b912394p-5 / N / N / N, c1 = 0x1.ebfce50fac4f3p-3 / N / N,
+                 c2 = 0x1.62e42ff0c52d6p-1 / N, shift = 0x1.8p+52;
+    const double xd = x, z = inv_ln2_n * xd;
+    double kd = z + shift;
+    uint64_t ki;
+    memcpy(&ki, &kd, 8);
+    kd -= shift;
+    const double r = fma(inv_ln2_n, xd, -kd);
+    uint64_t t = kExp2fTab[ki % 32] + (ki << (52 - 5));
+    double s;
+    memcpy(&s, &t, 8);
+    const double zz = fma(c0, r, c1), r2 = r * r;
+    double y = fma(c2, r, 1.0);
+    y = fma(zz, r2, y);
+    return (float)(y * s);
+}
+
+/* bit patterns start, start+stride, ... (count of them): how many differ from libm expf */
+int64_t ce_ref_expf_mismatches(uint32_t start, uint32_t stride, int64_t count) {
+    int64_t bad = 0;
+    uint32_t u = start;
+    for (int64_t i = 0; i < count; ++i, u += stride) {
+        float x;
+        memcpy(&x, &u, 4);
+        const float ref = expf(x), got = ce_ref_expf(x);
+        if (isnan(ref) ? !isnan(got) : f32_bits(ref) != f32_bits(got)) ++bad;
+    }
+    return bad;
+}
+
+int ce_ref_xgb_predict_proba(const double *X, int64_t F, int32_t D, int64_t ld, const int64_t *node_off,
+                             const int32_t *left, const int32_t *right, const int32_t *split_idx,
+                             const float *split_cond, const uint8_t *default_left, const int32_t *tree_info,
+                             int32_t T, int32_t G, int32_t C, float base_margin, float *out) {
+    if (G < 1 || G > 64 || !(G == C || (G == 1 && C == 2))) return -1;
+    float preds[64];
+    for (int64_t r = 0; r < F; ++r) {
+        const double *x = X + r * ld;
+        for (int g = 0; g < G; ++g) preds[g] = base_margin;
+        for (int t = 0; t < T; ++t) {
+            const int64_t o = node_off[t];
+            int32_t nid = 0;
+            while (left[o + nid] != -1) {
+                const int32_t f = split_idx[o + nid];
+                if (f < 0 || f >= D) return -2;
+                const double v = x[f];
+                if (isnan(v)) nid = default_left[o + nid] ? left[o + nid] : right[o + nid];
+                else nid = ((float)v < split_cond[o + nid]) ? left[o + nid] : right[o + nid];
+            }
+            preds[tree_info[t]] += split_cond[o + nid];
+        }
+        float *p = out + r * C;
+        if (G == 1) {
+            const float p1 = 1.0f / (1.0f + ce_ref_expf(-preds[0]));
+            p[0] = 1.0f - p1;
+            p[1] = p1;
+        } else {
+            float mx = preds[0];
+            for (int g = 1; g < G; ++g)
+                if (preds[g] > mx) mx = preds[g];
+            float wsum = 0.0f;
+            for (int g = 0; g < G; ++g) {
+                p[g] = ce_ref_expf(preds[g] - mx);
+                wsum += p[g];
+            }
+            for (int g = 0; g < G; ++g) p[g] /= wsum;
+        }
+    }
+    return 0;
+}
+
+/* got[k] = an implementation's expf of bit pattern start + k: how many differ from libm's expf */
+int64_t ce_ref_expf_check(const float *got, uint32_t start, int64_t count) {
+    int64_t bad = 0;
+    for (int64_t k = 0; k < count; ++k) {
+        const uint32_t u = start + (uint32_t)k;
+        float x;
+        memcpy(&x, &u, 4);
+        const float ref = expf(x);
+        if (isnan(ref) ? !isnan(got[k]) : f32_bits(ref) != f32_bits(got[k])) ++bad;
+    }
+    return bad;
+}

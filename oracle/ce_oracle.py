@@ -315,3 +315,136 @@ def oracle_select_mix(P, hc_table, q, layout="MNC"):
     ent_mc = oracle_committee_entropy(P, layout)
     ent_hc = oracle_table_entropy(hc_table)
     return oracle_topq(np.concatenate([ent_mc, ent_hc]), q)
+
+
+# ---------------------------------------------------------------------------
+# XGBClassifier.predict_proba (xgboost 1.3.3 predictor,
+# restated -- see the ce_oracle.c section for the algorithm and why parity is
+# unpinned against xgboost itself, which is absent from this image)
+# ---------------------------------------------------------------------------
+def _xgb_trees(model):
+    """(node_off, left, right, split, cond, default_left, tree_info, G, C, base_margin)
+    from an xgboost JSON model dict, the model's own node arrays concatenated."""
+    lrn = model["learner"]
+    m = lrn["gradient_booster"]["model"]
+    objective = lrn.get("objective", {}).get("name", "multi:softprob")
+    nc = int(lrn["learner_model_param"].get("num_class", "0"))
+    G, C = (1, 2) if objective == "binary:logistic" else (nc, nc)
+    bs = np.float32(float(lrn["learner_model_param"]["base_score"]))
+    if objective == "binary:logistic":
+        base = np.float32(-_libm_logf(np.float32(np.float32(1.0) / bs - np.float32(1.0))))
+    else:
+        base = bs
+    trees = m["trees"]
+    sizes = [len(t["left_children"]) for t in trees]
+    node_off = np.zeros(len(trees) + 1, dtype=np.int64)
+    node_off[1:] = np.cumsum(sizes)
+    cat = lambda key, dt: np.ascontiguousarray(  # noqa: E731
+        np.concatenate([np.asarray(t[key], dtype=dt) for t in trees]) if trees else np.zeros(0, dt))
+    return (node_off, cat("left_children", np.int32), cat("right_children", np.int32),
+            cat("split_indices", np.int32), cat("split_conditions", np.float32),
+            np.ascontiguousarray(np.concatenate([[bool(v) for v in t["default_left"]] for t in trees]).astype(np.uint8)),
+            np.ascontiguousarray(m["tree_info"], dtype=np.int32), G, C, base)
+
+
+_LIBM = None
+
+
+def _libm():
+    global _LIBM
+    if _LIBM is None:
+        import ctypes.util
+        _LIBM = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+        for fn in ("expf", "logf"):
+            getattr(_LIBM, fn).restype = ctypes.c_float
+            getattr(_LIBM, fn).argtypes = [ctypes.c_float]
+    return _LIBM
+
+
+def _libm_logf(x):
+    return np.float32(_libm().logf(ctypes.c_float(x)))
+
+
+def libm_expf(x):
+    """The host C library's expf (what libxgboost calls)."""
+    return np.float32(_libm().expf(ctypes.c_float(x)))
+
+
+def oracle_xgb_predict_proba(X, model):
+    """ce_oracle.c's restated predictor on X [F, D] (f64 or f32) -> [F, C] float32."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    F, D = X.shape
+    node_off, left, right, split, cond, dl, tinfo, G, C, base = _xgb_trees(model)
+    out = np.empty((F, C), dtype=np.float32)
+    L = lib()
+    vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+    L.ce_ref_xgb_predict_proba.argtypes = [vp, i64, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
+                                           ctypes.c_float, vp]
+    rc = L.ce_ref_xgb_predict_proba(_ptr(X), F, D, D, _ptr(node_off), _ptr(left), _ptr(right), _ptr(split),
+                                    _ptr(cond), _ptr(dl), _ptr(tinfo), len(tinfo), G, C, float(base), _ptr(out))
+    assert rc == 0, rc
+    return out
+
+
+def oracle_expf(x):
+    """The restated glibc expf (ce_ref_expf) elementwise."""
+    L = lib()
+    L.ce_ref_expf.restype = ctypes.c_float
+    L.ce_ref_expf.argtypes = [ctypes.c_float]
+    return np.array([L.ce_ref_expf(ctypes.c_float(v)) for v in np.asarray(x, np.float32).ravel()], np.float32)
+
+
+def oracle_expf_mismatches(start, stride, count):
+    """How many float bit patterns start + k*stride (k < count) the restated expf
+    gets different from libm's expf."""
+    L = lib()
+    L.ce_ref_expf_mismatches.restype = ctypes.c_int64
+    L.ce_ref_expf_mismatches.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64]
+    return int(L.ce_ref_expf_mismatches(start, stride, count))
+
+
+def ref_xgb_predict_proba_py(X, model):
+    """Pure-Python walk of the JSON model with numpy float32 arithmetic and the
+    host's libm expf (small cases only): an independent check of ce_oracle.c."""
+    lrn = model["learner"]
+    m = lrn["gradient_booster"]["model"]
+    _, _, _, _, _, _, tinfo, G, C, base = _xgb_trees(model)
+    X32 = np.asarray(X, dtype=np.float64).astype(np.float32)
+    out = np.empty((X32.shape[0], C), dtype=np.float32)
+    for r in range(X32.shape[0]):
+        preds = [np.float32(base)] * G
+        for t, tr in enumerate(m["trees"]):
+            nid = 0
+            while tr["left_children"][nid] != -1:
+                v = X32[r, tr["split_indices"][nid]]
+                if np.isnan(v):
+                    nid = tr["left_children"][nid] if tr["default_left"][nid] else tr["right_children"][nid]
+                elif v < np.float32(tr["split_conditions"][nid]):
+                    nid = tr["left_children"][nid]
+                else:
+                    nid = tr["right_children"][nid]
+            g = tinfo[t]
+            preds[g] = np.float32(preds[g] + np.float32(tr["split_conditions"][nid]))
+        if G == 1:
+            p1 = np.float32(np.float32(1.0) / np.float32(np.float32(1.0) + libm_expf(-preds[0])))
+            out[r] = [np.float32(1.0) - p1, p1]
+        else:
+            mx = preds[0]
+            for v in preds[1:]:
+                if v > mx:
+                    mx = v
+            e = [libm_expf(np.float32(v - mx)) for v in preds]
+            ws = np.float32(0.0)
+            for v in e:
+                ws = np.float32(ws + v)
+            out[r] = [np.float32(v / ws) for v in e]
+    return out
+
+
+def oracle_expf_check(got, start):
+    """Mismatches of got[k] (an expf of bit pattern start + k) against libm's expf."""
+    got = np.ascontiguousarray(got, dtype=np.float32)
+    L = lib()
+    L.ce_ref_expf_check.restype = ctypes.c_int64
+    L.ce_ref_expf_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64]
+    return int(L.ce_ref_expf_check(_ptr(got), start, got.size))

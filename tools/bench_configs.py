@@ -165,7 +165,7 @@ def cpu_reference_1thread(only):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="0,1,2,4,5,6")
+    ap.add_argument("--only", default="0,1,2,4,5,6,7")
     ap.add_argument("--cpu", action="store_true", help="also time the reference expressions on the host")
     args = ap.parse_args()
     only = {int(x) for x in args.only.split(",")}
@@ -234,6 +234,22 @@ def main():
             report(f"(f)4 GaussianNB predict_proba {F} frames x {D} f64", F, F * D * 8, t)
             t = timed(lambda: ops.sgd_predict_proba(X, coef, icpt), reps)
             report(f"(f)4 SGD(log) predict_proba {F} frames x {D} f64", F, F * D * 8, t)
+            del X
+    if 7 in only:  # §8(f)4: the xgb member, XGBClassifier(max_depth=5) x 100 rounds x 4 classes over 260 features
+        import numpy as np
+
+        from ce_amd.xgb import XgbForest, synthetic_model
+
+        D = 260
+        forest = XgbForest.from_json(synthetic_model(n_rounds=100, num_class=4, max_depth=5, num_feature=D))
+        depth, T = forest.pack()[3], len(forest.trees)
+        for F in (64_320, 4_000_000):
+            X = torch.randn((F, D), device="cuda", dtype=torch.float64, generator=g)
+            X[torch.rand((F, D), device="cuda", generator=g) < 0.01] = float("nan")
+            reps = 100 if F < 100_000 else 10
+            t = timed(lambda: ops.xgb_predict_proba(X, forest), reps)
+            report(f"(f)4 XGB predict_proba {F} frames x {D} f64, {T} trees depth {depth}", F, F * D * 8, t,
+                   {"node_steps_per_s": F * T * depth / t})
             del X
 
 
