@@ -205,7 +205,6 @@ def xgb_predict_proba(X, forest, out=None, out_dtype=torch.float32):
     if not isinstance(forest, XgbForest):
         forest = XgbForest.from_json(forest)
     F, D = X.shape
-    nodes, leaves, goff, depth = forest.device_arrays(X.device)
     if forest.max_feature() >= D:
         raise ValueError(f"the forest splits on feature {forest.max_feature()} but X has {D} columns")
     G, C = forest.n_groups, forest.n_classes
@@ -213,6 +212,7 @@ def xgb_predict_proba(X, forest, out=None, out_dtype=torch.float32):
         out = torch.empty((F, C), dtype=out_dtype, device=X.device)
     if out.dim() != 2 or out.shape[0] != F or out.shape[1] < C or out.stride(1) != 1 or out.dtype not in _DT:
         raise ValueError(f"out must be a float [{F}, >={C}] tensor with unit column stride")
+    nodes, leaves, goff, depth = forest.device_arrays(X.device)
     call("ce_xgb_predict_proba", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(nodes), _p(leaves), _p(goff), G, depth,
          float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0), _stream(X.device))
     return out

@@ -38,6 +38,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/ce.h"
 #include "ce_abi.hpp"
@@ -46,7 +47,6 @@ namespace ce {
 
 constexpr int kXgbTile = 64;      // frames per block
 constexpr int kXgbPad = 65;       // LDS column stride (floats)
-constexpr int kXgbIlp = 8;        // trees walked together per wave
 constexpr int kXgbMaxDepth = 10;  // packed depth limit (2^10 leaves per tree)
 constexpr int kXgbMaxFeat = 512;
 constexpr int kXgbMaxGroups = 8;
@@ -99,120 +99,221 @@ struct XgbArgs {
     int64_t F;
     int D;
     int64_t ld;
-    const uint2* nodes;   // [T][NI]
-    const float* leaves;  // [T][NI + 1]
-    const int32_t* goff;  // [G + 1]
-    int depth, NI, G, C;
+    int G, C, S;  // groups, classes, waves per group
     float base;
     void* out;
     int64_t ldo;
 };
 
-template <int XDT, int ODT>
-__global__ __launch_bounds__(256) void k_xgb_proba(XgbArgs a) {
+// Stage frames [f0, f0 + 64) of X as float32 into LDS, feature-major [D][65]
+// (consecutive threads take consecutive features of a row: conflict-free
+// writes); rows past the end repeat the last frame.  8 loads in flight.
+// Returns whether this thread staged a NaN (missing value).
+template <int XDT>
+__device__ __forceinline__ bool stage_tile(const void* X, int64_t F, int D, int64_t ld, int64_t f0, int nf,
+                                           float* xs) {
+    const int total = kXgbTile * D;
+    bool has_nan = false;
+    for (int e0 = threadIdx.x; e0 < total; e0 += blockDim.x * 8) {
+        float v[8];
+        int dst[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * blockDim.x;
+            const int ec = e < total ? e : total - 1;
+            const int r = ec / D, f = ec - r * D;
+            const int64_t row = f0 + (r < nf ? r : nf - 1);
+            if constexpr (XDT == CE_F64)
+                v[u] = (float)static_cast<const double*>(X)[row * ld + f];
+            else
+                v[u] = static_cast<const float*>(X)[row * ld + f];
+            dst[u] = e < total ? f * kXgbPad + r : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (dst[u] >= 0) {
+                xs[dst[u]] = v[u];
+                has_nan |= __builtin_isnan(v[u]);
+            }
+    }
+    return has_nan;
+}
+
+// The objective's transform of the G margins mg[g * 64 + lane] of frame f0 +
+// lane, written to out (wave 0, one frame per lane).
+template <int ODT>
+__device__ __forceinline__ void transform_store(const float* mg, int G, int C, int64_t f0, int nf, void* out,
+                                                int64_t ldo) {
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x >= 64 || lane >= nf) return;
+    const int64_t fr = f0 + lane;
+    float p[kXgbMaxGroups];
+    if (G == 1) {  // binary:logistic -> [1 - p, p]
+        const float m = mg[lane];
+        const float p1 = 1.0f / (1.0f + glibc_expf(-m));
+        p[0] = 1.0f - p1;
+        p[1] = p1;
+    } else {  // multi:softprob -> common::Softmax
+        float mx = mg[lane];
+        for (int g = 1; g < G; ++g) {
+            const float v = mg[g * 64 + lane];
+            if (v > mx) mx = v;
+        }
+        float wsum = 0.0f;
+        for (int g = 0; g < G; ++g) {
+            p[g] = glibc_expf(mg[g * 64 + lane] - mx);
+            wsum += p[g];
+        }
+        for (int g = 0; g < G; ++g) p[g] /= wsum;
+    }
+    for (int c = 0; c < C; ++c) {
+        if constexpr (ODT == CE_F64)
+            static_cast<double*>(out)[fr * ldo + c] = (double)p[c];
+        else
+            static_cast<float*>(out)[fr * ldo + c] = p[c];
+    }
+}
+
+// ---- forest layouts: leaf values of 8 consecutive trees of one group --------
+// MISS: the tile holds a missing value somewhere (block-uniform).  Without
+// one, "missing -> default child" never fires and the test is !(x < split).
+
+// Perfect-tree walk (any tree of depth <= 10): 8 trees walked together, so 8
+// independent node-gather -> LDS-read -> compare chains are in flight.
+struct WalkForest {
+    const uint2* nodes;   // [T][NI] {feature | default_left << 31, split_cond bits}
+    const float* leaves;  // [T][NI + 1]
+    const int32_t* goff;  // [G + 1]
+    int depth, NI;
+
+    struct Cursor {
+        const WalkForest* f;
+        template <bool MISS>
+        __device__ __forceinline__ void leaves8(const float* xs, int D, int t0, int t1, int lane, float (&v)[8]) {
+            f->template leaves8<MISS>(xs, D, t0, t1, lane, v);
+        }
+    };
+    __device__ __forceinline__ Cursor cursor(int) const { return Cursor{this}; }
+
+    template <bool MISS>
+    __device__ __forceinline__ void leaves8(const float* xs, int D, int t0, int t1, int lane, float (&v)[8]) const {
+        int idx[8];
+        const uint2* tn[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int t = t0 + j < t1 ? t0 + j : t1 - 1;
+            tn[j] = nodes + (int64_t)t * NI;
+            idx[j] = 0;
+        }
+        for (int lev = 0; lev < depth; ++lev) {
+            uint2 nd[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) nd[j] = tn[j][idx[j]];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int ft = min((int)(nd[j].x & 0x7fffffffu), D - 1);  // packer checks < D
+                const float x = xs[ft * kXgbPad + lane];
+                const float th = __uint_as_float(nd[j].y);
+                bool right;
+                if constexpr (MISS)  // missing -> default child; else fvalue < split_cond ? left : right
+                    right = __builtin_isnan(x) ? (nd[j].x >> 31) == 0u : !(x < th);
+                else
+                    right = !(x < th);
+                idx[j] = 2 * idx[j] + 1 + (right ? 1 : 0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int t = t0 + j < t1 ? t0 + j : t1 - 1;
+            v[j] = leaves[(int64_t)t * (NI + 1) + (idx[j] - NI)];
+        }
+    }
+};
+
+// ---- one block per 64-frame tile: G x S waves ------------------------------
+// Wave (g, s) takes a contiguous run of group g's trees: s = 0 the head, its
+// leaves added straight into the margin (a batch's leaf loads are added after
+// the next batch is evaluated, hiding their latency); s >= 1 one of the S - 1
+// tail chunks of at most kXgbChunk trees, whose leaf values wait in registers.
+// S ordered phases then hand the margin on through LDS (phase s: wave (g, s)
+// adds its leaves in model order), so preds[g] is exactly the reference's
+// sequential float chain while S times as many waves hide the latency.
+constexpr int kXgbChunk = 24;
+
+template <class L, bool MISS>
+__device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, const float* xs, float* mg, int g,
+                                              int s, int lane) {
+    const int k0 = fl.goff[g], k1 = fl.goff[g + 1], n = k1 - k0, S = a.S;
+    const int c = min(kXgbChunk, (n + S - 1) / S);
+    const int head_end = max(k0, k1 - (S - 1) * c);
+    float m = a.base;
+    float lv[kXgbChunk];
+    int cnt = 0;
+    auto cur = fl.cursor(a.G);
+    if (s == 0) {
+        float pend[8];
+        int npend = 0;
+        for (int k = k0; k < head_end; k += 8) {
+            float v[8];
+            cur.template leaves8<MISS>(xs, a.D, k, head_end, lane, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < npend) m += pend[j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pend[j] = v[j];
+            npend = min(8, head_end - k);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < npend) m += pend[j];
+    } else {
+        const int lo = head_end + (s - 1) * c, hi = min(k1, lo + c);
+        cnt = max(0, hi - lo);
+#pragma unroll
+        for (int b = 0; b < kXgbChunk / 8; ++b) {
+            if (b * 8 < cnt) {
+                float v[8];
+                cur.template leaves8<MISS>(xs, a.D, lo + b * 8, hi, lane, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) lv[b * 8 + j] = v[j];
+            }
+        }
+    }
+    for (int ph = 0; ph < S; ++ph) {
+        if (s == ph) {
+            if (s > 0) m = mg[g * 64 + lane];
+#pragma unroll
+            for (int i = 0; i < kXgbChunk; ++i)
+                if (i < cnt) m += lv[i];
+            mg[g * 64 + lane] = m;
+        }
+        __syncthreads();
+    }
+}
+
+template <int XDT, int ODT, class L>
+__device__ __forceinline__ void xgb_tile(const XgbArgs& a, const L& fl) {
     extern __shared__ float xsm[];
-    float* xs = xsm;                          // [D][kXgbPad]
-    float* mg = xsm + a.D * kXgbPad;          // [G][64] final margins
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    float* xs = xsm;                  // [D][kXgbPad]
+    float* mg = xsm + a.D * kXgbPad;  // [G][64] margins
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = w / a.S, s = w - g * a.S;
     const int64_t f0 = (int64_t)blockIdx.x * kXgbTile;
     const int nf = (int)min<int64_t>(kXgbTile, a.F - f0);
+    const bool has_nan = stage_tile<XDT>(a.X, a.F, a.D, a.ld, f0, nf, xs);
+    if (__syncthreads_or(has_nan))
+        split_margins<L, true>(a, fl, xs, mg, g, s, lane);
+    else
+        split_margins<L, false>(a, fl, xs, mg, g, s, lane);
+    transform_store<ODT>(mg, a.G, a.C, f0, nf, a.out, a.ldo);
+}
 
-    // ---- stage the tile: element e = (row r, feature f), 8 loads in flight ----
-    {
-        const int total = kXgbTile * a.D;
-        for (int e0 = threadIdx.x; e0 < total; e0 += blockDim.x * 8) {
-            float v[8];
-            int dst[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = e0 + u * blockDim.x;
-                const int ec = e < total ? e : total - 1;
-                const int r = ec / a.D, f = ec - r * a.D;
-                const int64_t row = f0 + (r < nf ? r : nf - 1);  // pad rows repeat the last frame
-                if constexpr (XDT == CE_F64)
-                    v[u] = (float)static_cast<const double*>(a.X)[row * a.ld + f];
-                else
-                    v[u] = static_cast<const float*>(a.X)[row * a.ld + f];
-                dst[u] = e < total ? f * kXgbPad + r : -1;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (dst[u] >= 0) xs[dst[u]] = v[u];
-        }
-    }
-    __syncthreads();
-
-    // ---- wave w: groups w, w + nw, ...; 8 trees of a group walked together ----
-    const int NL = a.NI + 1;
-    for (int g = w; g < a.G; g += nw) {
-        const int k0 = a.goff[g], k1 = a.goff[g + 1];
-        float m = a.base;
-        for (int k = k0; k < k1; k += kXgbIlp) {
-            int idx[kXgbIlp];
-            const uint2* tn[kXgbIlp];
-#pragma unroll
-            for (int j = 0; j < kXgbIlp; ++j) {
-                const int kk = k + j < k1 ? k + j : k1 - 1;
-                tn[j] = a.nodes + (int64_t)kk * a.NI;
-                idx[j] = 0;
-            }
-            for (int lev = 0; lev < a.depth; ++lev) {
-                uint2 nd[kXgbIlp];
-#pragma unroll
-                for (int j = 0; j < kXgbIlp; ++j) nd[j] = tn[j][idx[j]];
-#pragma unroll
-                for (int j = 0; j < kXgbIlp; ++j) {
-                    const int ft = min((int)(nd[j].x & 0x7fffffffu), a.D - 1);  // packer checks < D; clamp keeps LDS in range
-                    const float x = xs[ft * kXgbPad + lane];
-                    // missing -> default child; else fvalue < split_cond ? left : right
-                    const bool right = __builtin_isnan(x) ? (nd[j].x >> 31) == 0u
-                                                         : !(x < __uint_as_float(nd[j].y));
-                    idx[j] = 2 * idx[j] + 1 + (right ? 1 : 0);
-                }
-            }
-            float lv[kXgbIlp];
-#pragma unroll
-            for (int j = 0; j < kXgbIlp; ++j) {
-                const int kk = k + j < k1 ? k + j : k1 - 1;
-                lv[j] = a.leaves[(int64_t)kk * NL + (idx[j] - a.NI)];
-            }
-#pragma unroll
-            for (int j = 0; j < kXgbIlp; ++j)
-                if (k + j < k1) m += lv[j];  // preds[g] += leaf, model order
-        }
-        mg[g * 64 + lane] = m;
-    }
-    __syncthreads();
-
-    // ---- transform (wave 0, one frame per lane) ----
-    if (w == 0 && lane < nf) {
-        const int64_t fr = f0 + lane;
-        float p[kXgbMaxGroups];
-        if (a.G == 1) {  // binary:logistic -> [1 - p, p]
-            const float m = mg[lane];
-            const float p1 = 1.0f / (1.0f + glibc_expf(-m));
-            p[0] = 1.0f - p1;
-            p[1] = p1;
-        } else {  // multi:softprob -> common::Softmax
-            float mx = mg[lane];
-            for (int g = 1; g < a.G; ++g) {
-                const float v = mg[g * 64 + lane];
-                if (v > mx) mx = v;
-            }
-            float wsum = 0.0f;
-            for (int g = 0; g < a.G; ++g) {
-                p[g] = glibc_expf(mg[g * 64 + lane] - mx);
-                wsum += p[g];
-            }
-            for (int g = 0; g < a.G; ++g) p[g] /= wsum;
-        }
-        for (int c = 0; c < a.C; ++c) {
-            if constexpr (ODT == CE_F64)
-                static_cast<double*>(a.out)[fr * a.ldo + c] = (double)p[c];
-            else
-                static_cast<float*>(a.out)[fr * a.ldo + c] = p[c];
-        }
-    }
+template <int XDT, int ODT>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_xgb_walk(XgbArgs a, const uint2* __restrict__ nodes,
+                                                   const float* __restrict__ leaves, const int32_t* __restrict__ goff,
+                                                   int depth) {
+    xgb_tile<XDT, ODT>(a, WalkForest{nodes, leaves, goff, depth, (1 << depth) - 1});
 }
 
 __global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
@@ -229,30 +330,51 @@ extern "C" size_t ce_xgb_lds_bytes(int32_t D, int32_t G) {
     return (size_t)D * kXgbPad * sizeof(float) + (size_t)std::max(G, 1) * 64 * sizeof(float);
 }
 
+// waves per group: fill a 16-wave block
+static int xgb_splits(int G) { return std::max(1, 16 / G); }
+
+template <class LaunchFn>
+static void xgb_dispatch(ce_dtype x_dt, ce_dtype out_dt, LaunchFn&& fn) {
+    if (x_dt == CE_F64)
+        out_dt == CE_F64 ? fn(std::integral_constant<int, CE_F64>(), std::integral_constant<int, CE_F64>())
+                         : fn(std::integral_constant<int, CE_F64>(), std::integral_constant<int, CE_F32>());
+    else
+        out_dt == CE_F64 ? fn(std::integral_constant<int, CE_F32>(), std::integral_constant<int, CE_F64>())
+                         : fn(std::integral_constant<int, CE_F32>(), std::integral_constant<int, CE_F32>());
+}
+
+static int xgb_check(const void* X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld, int32_t G, int32_t C,
+                     const void* out, ce_dtype out_dt, int64_t ld_out) {
+    if (F < 0 || D < 1 || D > kXgbMaxFeat || ld < D || G < 1 || G > kXgbMaxGroups || ld_out < C ||
+        !(G == C || (G == 1 && C == 2)))
+        return fail(CE_EINVAL, "bad XGB shapes F=%lld D=%d G=%d C=%d", (long long)F, D, G, C);
+    if ((x_dt != CE_F32 && x_dt != CE_F64) || (out_dt != CE_F32 && out_dt != CE_F64))
+        return fail(CE_EINVAL, "XGB dtypes must be F32 or F64");
+    if (F > 0 && (!X || !out)) return fail(CE_EINVAL, "null pointer");
+    return CE_OK;
+}
+
+template <class K, class... Args>
+static void xgb_launch(K kern, int64_t F, size_t lds, int threads, ce_stream_t stream, Args... args) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((F + kXgbTile - 1) / kXgbTile)), dim3(threads), lds,
+                       (hipStream_t)stream, args...);
+}
+
 extern "C" int ce_xgb_predict_proba(const void* X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld,
                                     const uint32_t* nodes, const float* leaves, const int32_t* group_offsets,
                                     int32_t G, int32_t depth, float base_margin, int32_t C, void* out,
                                     ce_dtype out_dt, int64_t ld_out, ce_stream_t stream) {
-    if (F < 0 || D < 1 || D > kXgbMaxFeat || ld < D || depth < 0 || depth > kXgbMaxDepth || G < 1 ||
-        G > kXgbMaxGroups || ld_out < C || !(G == C || (G == 1 && C == 2)))
-        return fail(CE_EINVAL, "bad XGB shapes F=%lld D=%d depth=%d G=%d C=%d", (long long)F, D, depth, G, C);
-    if ((x_dt != CE_F32 && x_dt != CE_F64) || (out_dt != CE_F32 && out_dt != CE_F64))
-        return fail(CE_EINVAL, "XGB dtypes must be F32 or F64");
-    if ((F > 0 && (!X || !out)) || !nodes || !leaves || !group_offsets) return fail(CE_EINVAL, "null pointer");
+    if (int rc = xgb_check(X, x_dt, F, D, ld, G, C, out, out_dt, ld_out)) return rc;
+    if (depth < 0 || depth > kXgbMaxDepth) return fail(CE_EINVAL, "XGB depth %d outside [0, %d]", depth, kXgbMaxDepth);
+    if (!nodes || !leaves || !group_offsets) return fail(CE_EINVAL, "null pointer");
     if (F == 0) return CE_OK;
-    XgbArgs a{X, F, D, ld, reinterpret_cast<const uint2*>(nodes), leaves, group_offsets,
-              depth, (1 << depth) - 1, G, C, base_margin, out, ld_out};
-    const size_t lds = ce_xgb_lds_bytes(D, G);
-    const int threads = 64 * std::min(G, 4);
-    const dim3 grid((unsigned)((F + kXgbTile - 1) / kXgbTile));
-    auto launch = [&](auto kern) {
-        if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, grid, dim3(threads), lds, (hipStream_t)stream, a);
-    };
-    if (x_dt == CE_F64)
-        out_dt == CE_F64 ? launch(k_xgb_proba<CE_F64, CE_F64>) : launch(k_xgb_proba<CE_F64, CE_F32>);
-    else
-        out_dt == CE_F64 ? launch(k_xgb_proba<CE_F32, CE_F64>) : launch(k_xgb_proba<CE_F32, CE_F32>);
+    const int S = xgb_splits(G);
+    const XgbArgs a{X, F, D, ld, G, C, S, base_margin, out, ld_out};
+    xgb_dispatch(x_dt, out_dt, [&](auto xd, auto od) {
+        xgb_launch(k_xgb_walk<decltype(xd)::value, decltype(od)::value>, F, ce_xgb_lds_bytes(D, G), 64 * G * S,
+                   stream, a, reinterpret_cast<const uint2*>(nodes), leaves, group_offsets, depth);
+    });
     return check_launch("ce_xgb_predict_proba");
 }
 

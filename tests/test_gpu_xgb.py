@@ -60,15 +60,30 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("nan", [0.03, 0.0], ids=["missing", "dense"])
 @pytest.mark.parametrize("name,kw,F", CASES, ids=[c[0] for c in CASES])
-def test_xgb_bit_exact(ce, name, kw, F):
+def test_xgb_bit_exact(ce, name, kw, F, nan):
+    """With missing values (every tile takes the default-direction path) and
+    without (the single-compare path)."""
     model = synthetic_model(**kw)
-    X = frames(F, kw["num_feature"], seed=F, model=model)
-    exp = O.oracle_xgb_predict_proba(X, model)
     forest = XgbForest.from_json(model)
+    X = frames(F, kw["num_feature"], seed=F, nan=nan, model=model)
+    exp = O.oracle_xgb_predict_proba(X, model)
     got = ce.ops.xgb_predict_proba(dev(X), forest).cpu().numpy()
     assert got.dtype == np.float32
     assert np.array_equal(bits(got), bits(exp)), (np.argwhere(bits(got) != bits(exp))[:5], name)
+
+
+def test_xgb_sparse_missing_tiles(ce):
+    """A few NaN frames scattered over many tiles: tiles with and without a
+    missing value in one launch."""
+    kw = dict(n_rounds=40, num_class=4, max_depth=5, num_feature=260, seed=31)
+    model = synthetic_model(**kw)
+    X = frames(64 * 300 + 5, 260, seed=9, nan=0.0, model=model)
+    X[np.arange(7, X.shape[0], 997), np.arange(7, X.shape[0], 997) % 260] = np.nan
+    exp = O.oracle_xgb_predict_proba(X, model)
+    got = ce.ops.xgb_predict_proba(dev(X), XgbForest.from_json(model)).cpu().numpy()
+    assert np.array_equal(bits(got), bits(exp))
 
 
 def test_xgb_dtypes_and_strides(ce):

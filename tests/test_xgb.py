@@ -163,3 +163,4 @@ def test_ops_guard_without_gpu():
 
     with pytest.raises(ValueError, match="HIP device"):
         ops.xgb_predict_proba(torch.zeros((4, 10), dtype=torch.float64), synthetic_model(n_rounds=1, num_feature=10))
+

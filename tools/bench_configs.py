@@ -245,11 +245,14 @@ def main():
         depth, T = forest.pack()[3], len(forest.trees)
         for F in (64_320, 4_000_000):
             X = torch.randn((F, D), device="cuda", dtype=torch.float64, generator=g)
-            X[torch.rand((F, D), device="cuda", generator=g) < 0.01] = float("nan")
             reps = 100 if F < 100_000 else 10
-            t = timed(lambda: ops.xgb_predict_proba(X, forest), reps)
-            report(f"(f)4 XGB predict_proba {F} frames x {D} f64, {T} trees depth {depth}", F, F * D * 8, t,
-                   {"node_steps_per_s": F * T * depth / t})
+            for miss in (False, True):
+                if miss:  # one missing value per ~100 frames: most tiles take the default-direction path
+                    X[torch.rand((F, D), device="cuda", generator=g) < 1e-4] = float("nan")
+                t = timed(lambda: ops.xgb_predict_proba(X, forest), reps)
+                report(f"(f)4 XGB predict_proba {F} frames x {D} f64, {T} trees depth {depth}, "
+                       f"{'with' if miss else 'no'} missing values", F, F * D * 8, t,
+                       {"node_steps_per_s": F * T * depth / t})
             del X
 
 
