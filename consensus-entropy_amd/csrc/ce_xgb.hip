@@ -186,17 +186,21 @@ struct WalkForest {
     const int32_t* goff;  // [G + 1]
     int depth, NI;
 
-    struct Cursor {
-        const WalkForest* f;
-        template <bool MISS>
-        __device__ __forceinline__ void leaves8(const float* xs, int D, int t0, int t1, int lane, float (&v)[8]) {
-            f->template leaves8<MISS>(xs, D, t0, t1, lane, v);
-        }
-    };
-    __device__ __forceinline__ Cursor cursor(int) const { return Cursor{this}; }
-
     template <bool MISS>
-    __device__ __forceinline__ void leaves8(const float* xs, int D, int t0, int t1, int lane, float (&v)[8]) const {
+    static __device__ __forceinline__ bool go_right(uint2 nd, const float* xs, int D, int lane) {
+        const int ft = min((int)(nd.x & 0x7fffffffu), D - 1);  // packer checks < D
+        const float x = xs[ft * kXgbPad + lane];
+        const float th = __uint_as_float(nd.y);
+        if constexpr (MISS)  // missing -> default child; else fvalue < split_cond ? left : right
+            return __builtin_isnan(x) ? (nd.x >> 31) == 0u : !(x < th);
+        else
+            return !(x < th);
+    }
+
+    // Level 0 reads the wave-uniform root (a scalar load; its feature read is
+    // one LDS column); deeper levels gather per lane.
+    template <bool MISS>
+    __device__ __forceinline__ void leafidx8(const float* xs, int D, int t0, int t1, int lane, int (&li)[8]) const {
         int idx[8];
         const uint2* tn[8];
 #pragma unroll
@@ -205,36 +209,33 @@ struct WalkForest {
             tn[j] = nodes + (int64_t)t * NI;
             idx[j] = 0;
         }
-        for (int lev = 0; lev < depth; ++lev) {
+        if (depth >= 1) {
+            uint2 r[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] = tn[j][0];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) idx[j] = go_right<MISS>(r[j], xs, D, lane) ? 2 : 1;
+        }
+        for (int lev = 1; lev < depth; ++lev) {
             uint2 nd[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) nd[j] = tn[j][idx[j]];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int ft = min((int)(nd[j].x & 0x7fffffffu), D - 1);  // packer checks < D
-                const float x = xs[ft * kXgbPad + lane];
-                const float th = __uint_as_float(nd[j].y);
-                bool right;
-                if constexpr (MISS)  // missing -> default child; else fvalue < split_cond ? left : right
-                    right = __builtin_isnan(x) ? (nd[j].x >> 31) == 0u : !(x < th);
-                else
-                    right = !(x < th);
-                idx[j] = 2 * idx[j] + 1 + (right ? 1 : 0);
-            }
+            for (int j = 0; j < 8; ++j) idx[j] = 2 * idx[j] + 1 + (go_right<MISS>(nd[j], xs, D, lane) ? 1 : 0);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int t = t0 + j < t1 ? t0 + j : t1 - 1;
-            v[j] = leaves[(int64_t)t * (NI + 1) + (idx[j] - NI)];
-        }
+        for (int j = 0; j < 8; ++j) li[j] = idx[j] - NI;
     }
+    // leaf value of tree t at leaf index li
+    __device__ __forceinline__ float value(int t, int li) const { return leaves[(int64_t)t * (NI + 1) + li]; }
 };
 
 // ---- one block per 64-frame tile: G x S waves ------------------------------
 // Wave (g, s) takes a contiguous run of group g's trees: s = 0 the head, its
 // leaves added straight into the margin (a batch's leaf loads are added after
 // the next batch is evaluated, hiding their latency); s >= 1 one of the S - 1
-// tail chunks of at most kXgbChunk trees, whose leaf values wait in registers.
+// tail chunks of at most kXgbChunk trees, whose leaf indices wait in registers
+// (16 bits each) until the wave's phase.
 // S ordered phases then hand the margin on through LDS (phase s: wave (g, s)
 // adds its leaves in model order), so preds[g] is exactly the reference's
 // sequential float chain while S times as many waves hide the latency.
@@ -247,15 +248,17 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
     const int c = min(kXgbChunk, (n + S - 1) / S);
     const int head_end = max(k0, k1 - (S - 1) * c);
     float m = a.base;
-    float lv[kXgbChunk];
-    int cnt = 0;
-    auto cur = fl.cursor(a.G);
+    uint32_t packed[kXgbChunk / 2];  // tail waves: leaf indices, 16 bits each
+    int lo = 0, cnt = 0;
     if (s == 0) {
         float pend[8];
         int npend = 0;
         for (int k = k0; k < head_end; k += 8) {
+            int li[8];
+            fl.template leafidx8<MISS>(xs, a.D, k, head_end, lane, li);
             float v[8];
-            cur.template leaves8<MISS>(xs, a.D, k, head_end, lane, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = fl.value(k + j < head_end ? k + j : head_end - 1, li[j]);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 if (j < npend) m += pend[j];
@@ -267,26 +270,36 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
         for (int j = 0; j < 8; ++j)
             if (j < npend) m += pend[j];
     } else {
-        const int lo = head_end + (s - 1) * c, hi = min(k1, lo + c);
+        lo = head_end + (s - 1) * c;
+        const int hi = min(k1, lo + c);
         cnt = max(0, hi - lo);
 #pragma unroll
         for (int b = 0; b < kXgbChunk / 8; ++b) {
             if (b * 8 < cnt) {
-                float v[8];
-                cur.template leaves8<MISS>(xs, a.D, lo + b * 8, hi, lane, v);
+                int li[8];
+                fl.template leafidx8<MISS>(xs, a.D, lo + b * 8, hi, lane, li);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) lv[b * 8 + j] = v[j];
+                for (int j = 0; j < 8; j += 2) packed[b * 4 + j / 2] = (uint32_t)li[j] | ((uint32_t)li[j + 1] << 16);
             }
         }
     }
     for (int ph = 0; ph < S; ++ph) {
-        if (s == ph) {
-            if (s > 0) m = mg[g * 64 + lane];
+        if (s == ph && s > 0) {
+            m = mg[g * 64 + lane];
 #pragma unroll
-            for (int i = 0; i < kXgbChunk; ++i)
-                if (i < cnt) m += lv[i];
-            mg[g * 64 + lane] = m;
+            for (int b = 0; b < kXgbChunk / 8; ++b) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int i = b * 8 + j;
+                    v[j] = fl.value(lo + (i < cnt ? i : 0), (packed[i / 2] >> (16 * (i & 1))) & 0xffffu);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (b * 8 + j < cnt) m += v[j];
+            }
         }
+        if (s == ph) mg[g * 64 + lane] = m;
         __syncthreads();
     }
 }
