@@ -3,6 +3,7 @@
 # time-out ends the script -- nothing more runs on the GPU in that call).
 #   PHASE=check    pytest -m gpu, smoke(), bench.py (default line + A/B lines)
 #   PHASE=profile  rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
+#   PHASE=xgb      the same for the XGB member (tools/bench_configs.py --only 7)
 # Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -57,6 +58,13 @@ configs)  # kernel-trace stats of every secondary config + FETCH/WRITE passes of
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/write_wide" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" --only 4 > "$OUT/prof_write_wide.log" 2>&1
   step $? "write wide"
   ;;
-*) echo "PHASE must be check, ab, profile or configs" >&2; exit 2 ;;
+xgb)  # kernel-trace stats + FETCH_SIZE pass of the XGB member (bench_configs --only 7)
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof/xgb" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" --only 7 > "$OUT/prof_xgb.log" 2>&1
+  step $? "trace xgb"
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/fetch_xgb" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" --only 7 > "$OUT/prof_fetch_xgb.log" 2>&1
+  step $? "fetch xgb"
+  ;;
+*) echo "PHASE must be check, ab, profile, configs or xgb" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"

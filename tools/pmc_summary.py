@@ -91,3 +91,31 @@ if pmc:
     json.dump(pmc, open(os.path.join(out_dir, f"{tag}_wide_pmc.json"), "w"), indent=1)
     print("wide", json.dumps(pmc, indent=1)[:800])
 json.dump(traffic, open(traffic_path, "w"), indent=1)
+# the XGB member (tools/bench_configs.py --only 7, PHASE=xgb): per-dispatch-size
+# kernel time from the trace, FETCH_SIZE per launch (x2, gfx950 rule above)
+xdir = os.path.join(prof, "xgb")
+if os.path.isdir(xdir):
+    rows = list(csv.reader(open(os.path.join(xdir, "run_kernel_stats.csv"))))
+    head, body = rows[0], [r for r in rows[1:] if r[0].startswith("void ce::")]
+    with open(os.path.join(out_dir, f"{tag}_xgb_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(head)
+        w.writerows(body)
+    by_grid = {}
+    for r in csv.DictReader(open(os.path.join(xdir, "run_kernel_trace.csv"))):
+        if "k_xgb_walk" in r["Kernel_Name"]:
+            frames = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]) * 64
+            by_grid.setdefault(frames, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+    fetch = {}
+    path = os.path.join(prof, "fetch_xgb", "run_counter_collection.csv")
+    if os.path.exists(path):
+        for r in csv.DictReader(open(path)):
+            if "k_xgb_walk" in r["Kernel_Name"]:
+                frames = int(r["Grid_Size"]) // int(r["Workgroup_Size"]) * 64
+                fetch.setdefault(frames, []).append(float(r["Counter_Value"]) * 1024 * 2)
+    summary = {str(k): {"dispatches": len(v), "mean_ms": statistics.mean(v), "min_ms": min(v),
+                        "hbm_fetch_bytes_per_launch": statistics.mean(fetch[k]) if k in fetch else None,
+                        "algorithmic_bytes_per_launch": k * 260 * 8}
+               for k, v in sorted(by_grid.items())}
+    json.dump(summary, open(os.path.join(out_dir, f"{tag}_xgb_summary.json"), "w"), indent=1)
+    print("xgb", json.dumps(summary, indent=1))
