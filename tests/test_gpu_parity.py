@@ -611,3 +611,19 @@ def test_lds_dma_stream_instantiations(ce, dt, C, M):
     assert np.array_equal(idx_np(idx), exp)
     _, idx = ce.ops.select_mc(Pd, 64, "NMC")
     assert np.array_equal(idx_np(idx), O.oracle_select_mc(host, 64, "NMC")[1])
+
+
+def test_gnb_widest_shape(ce):
+    """GaussianNB at the ABI's limits (C = 8 classes, D = 512 features: 96 KB of
+    theta / var / 1/var in LDS) against the restatement, with variances spread
+    over 12 decades (the reciprocal-corrected division)."""
+    from oracle.ce_oracle import ref_gnb_predict_proba
+
+    rng = np.random.default_rng(512)
+    C, D = 8, 512
+    theta = rng.normal(0, 1, (C, D))
+    var = 10.0 ** rng.uniform(-6, 6, (C, D))
+    prior = rng.dirichlet(np.ones(C))
+    X = theta[rng.integers(0, C, 3000)] + rng.normal(0, 1, (3000, D)) * np.sqrt(var[0])
+    got = ce.ops.gnb_predict_proba(dev(X), theta, var, prior).cpu().numpy()
+    np.testing.assert_allclose(got, ref_gnb_predict_proba(X, theta, var, prior), rtol=1e-10, atol=1e-300)
