@@ -16,7 +16,8 @@
 //     p = 1 / (1 + expf(-m)), returned as [1 - p, p] (sklearn.py:1027-1029).
 //   * expf is glibc's (>= 2.27, the x86-64 FMA ifunc variant): restated below
 //     and verified bit-identical to the host's libm on all 2^32 floats
-//     (tests/test_oracle.py, tests/test_gpu_parity.py).
+//     (tests/test_xgb.py on a dense stride, tests/test_gpu_xgb.py exhaustively
+//     on the device).
 //
 // Layout (packed on the host by ce_amd.xgb.XgbForest): every tree is padded to
 // a perfect binary tree of the forest's maximum depth d (an early leaf's
@@ -27,13 +28,13 @@
 //   nodes  [T][2^d - 1] x {feature | default_left << 31, split_cond bits}
 //   leaves [T][2^d] f32
 //
-// Kernel: one block per 64-frame tile.  The tile's features are staged ONCE as
-// float32 in LDS, feature-major [D][65] (lane = frame: a wave's feature reads
-// hit 64 different rows of one column).  Wave w owns the groups g = w, w+4
-// (no cross-wave exchange: each group's margin is one lane-private float
-// chain, added in model order), walking 8 trees at a time so 8 independent
-// node-load -> LDS-read -> compare chains are in flight per lane.  Bound:
-// X bytes from HBM (D * sizeof(x) per frame) vs. T * d node steps per frame.
+// Kernel (k_xgb_walk): one block of G x S waves per 64-frame tile.  The tile's
+// features are staged ONCE as float32 in LDS, feature-major [D][65] (lane =
+// frame).  Each group's trees are split over S waves whose partial chains are
+// joined in model order (split_margins); every wave walks 8 trees at a time so
+// 8 independent node-gather -> LDS-read -> compare chains are in flight per
+// lane.  Bound: latency of those chains (X bytes from HBM, D * sizeof(x) per
+// frame, are read once; T * d node steps per frame).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
