@@ -1299,6 +1299,12 @@ extern "C" int ce_sgd_predict_proba(const double* X, int64_t F, int32_t D, int64
     if (F == 0) return CE_OK;
     SgdArgs a{X, F, D, ld, coef, intercept, K, C, out, ld_out};
     const size_t lds = (size_t)K * D * sizeof(double);
+    if (D == 260 && ld == 260 && K == 4 && C == 4 && ((uintptr_t)X & 15) == 0) {
+        // the reference's contiguous rows: coalesced 16-B span loads; 76 KB LDS -> 2 blocks per CU, one resident wave of blocks
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(F, 32), 512));
+        hipLaunchKernelGGL((k_sgd_span260<4>), dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+        return check_launch("ce_sgd_predict_proba");
+    }
     with_nx(D, [&](auto nx) {
         hipLaunchKernelGGL((k_sgd_proba8<decltype(nx)::value>), dim3(member_grid8(F)), dim3(256), lds,
                            (hipStream_t)stream, a);

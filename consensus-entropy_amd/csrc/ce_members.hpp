@@ -216,6 +216,18 @@ __global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
     }
 }
 
+// Lane j's partial dot product -> the group's d (butterfly) -> expit(d + b).
+__device__ __forceinline__ double sgd_expit(double d, double b) {
+    d = d + __shfl_xor(d, 1);
+    d = d + __shfl_xor(d, 2);
+    d = d + __shfl_xor(d, 4);
+    d += b;
+    return 1.0 / (1.0 + exp(-d));  // scipy.special.expit
+}
+
+template <int KR>
+__device__ __forceinline__ void sgd_store(const SgdArgs& a, double (&p)[KR], int K, int64_t fr, int j);
+
 // SGDClassifier(loss='log'), 8 lanes per frame; coef in LDS.
 template <int NX>
 __global__ __launch_bounds__(256) void k_sgd_proba8(SgdArgs a) {
@@ -241,27 +253,90 @@ __global__ __launch_bounds__(256) void k_sgd_proba8(SgdArgs a) {
                 const int f = 8 * m + j;
                 if (f < a.D) d = fma(x[m], msm[c * a.D + f], d);
             }
-            d = d + __shfl_xor(d, 1);
-            d = d + __shfl_xor(d, 2);
-            d = d + __shfl_xor(d, 4);
-            d += a.intercept[c];
-            p[c] = 1.0 / (1.0 + exp(-d));  // scipy.special.expit
+            p[c] = sgd_expit(d, a.intercept[c]);
         }
-        if (a.K == 1) {
-            p[1] = p[0];
-            p[0] = 1.0 - p[1];
-        } else {
-            double s = -0.0;
-            for (int c = 0; c < a.K; ++c) s += p[c];
-            s = 0.0 + s;
-            for (int c = 0; c < a.K; ++c) p[c] /= s;
+        sgd_store(a, p, a.K, fr, j);
+    }
+}
+
+// The OvR normalisation (or the binary [1 - p, p]) and the store of lane j's class.
+template <int KR>
+__device__ __forceinline__ void sgd_store(const SgdArgs& a, double (&p)[KR], int K, int64_t fr, int j) {
+    if (K == 1) {
+        p[1] = p[0];
+        p[0] = 1.0 - p[1];
+    } else {
+        double s = -0.0;
+        for (int c = 0; c < K; ++c) s += p[c];
+        s = 0.0 + s;
+        for (int c = 0; c < K; ++c) p[c] /= s;
+    }
+    if (fr < a.F && j < a.C) {
+        double v = 0.0;
+        for (int c = 0; c < a.C; ++c)
+            if (c == j) v = p[c];
+        a.out[fr * a.ldo + j] = v;
+    }
+}
+
+// SGD for the reference's contiguous 260-feature rows (ld == D == 260, K == C
+// == KC): a wave's 8 frames are one contiguous 16,640-B span, fetched one span
+// ahead with 16-B non-temporal loads (1 KiB per instruction, fully coalesced,
+// instead of 8 rows x 64 B per 8-B load) and transposed through a wave-private
+// LDS slot (rows padded to 264 doubles) into k_sgd_proba8's 8-lanes-per-frame
+// layout -- the same FMA chains and butterfly, so the same bits.
+template <int KC>
+__global__ __launch_bounds__(256) void k_sgd_span260(SgdArgs a) {
+    constexpr int D = 260, RP = 264, NX = 33, SPAN = 8 * D / 2, NCH = (SPAN + 63) / 64;  // 1040 chunks, 17 loads
+    __shared__ __attribute__((aligned(16))) double cf[KC * D];
+    __shared__ __attribute__((aligned(16))) double xs[4][8 * RP];
+    for (int t = threadIdx.x; t < KC * D; t += blockDim.x) cf[t] = a.coef[t];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 7, g = lane >> 3, w = threadIdx.x >> 6;
+    const int64_t nchunks = a.F * (D / 2);
+    const f64x2* X2 = reinterpret_cast<const f64x2*>(a.X);
+    const int64_t step = (int64_t)gridDim.x * 32;
+    double* xw = xs[w];
+    f64x2 buf[NCH];
+    int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 8;
+    auto fetch = [&](int64_t fb) {
+        const int64_t c0 = fb * (D / 2);
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            const int c = k * 64 + lane;
+            if (c < SPAN && c0 + c < nchunks) buf[k] = __builtin_nontemporal_load(X2 + c0 + c);
         }
-        if (fr < a.F && j < a.C) {
-            double v = 0.0;
-            for (int c = 0; c < a.C; ++c)
-                if (c == j) v = p[c];
-            a.out[fr * a.ldo + j] = v;
+    };
+    if (f0 < a.F) fetch(f0);
+    for (; f0 < a.F; f0 += step) {
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            const int c = k * 64 + lane;
+            if (c < SPAN) {
+                const int r = (2 * c) / D, col = 2 * c - r * D;  // D even: a chunk never straddles rows
+                *reinterpret_cast<f64x2*>(xw + r * RP + col) = buf[k];
+            }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double x[NX];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) x[m] = (m < NX - 1 || j < D - 8 * (NX - 1)) ? xw[g * RP + 8 * m + j] : 0.0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // every lane's reads precede the next span's writes
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (f0 + step < a.F) fetch(f0 + step);
+        double p[KC > 1 ? KC : 2];
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+            double d = 0.0;
+#pragma unroll
+            for (int m = 0; m < NX; ++m)
+                if (m < NX - 1 || j < D - 8 * (NX - 1)) d = fma(x[m], cf[c * D + 8 * m + j], d);
+            p[c] = sgd_expit(d, a.intercept[c]);
+        }
+        sgd_store(a, p, KC, f0 + g, j);
     }
 }
 

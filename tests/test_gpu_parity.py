@@ -559,6 +559,22 @@ def test_member_inference_vs_restatement(ce):
     np.testing.assert_allclose(got, ref_sgd_predict_proba(Xt, sgd.coef_[:1], sgd.intercept_[:1]), rtol=1e-10)
 
 
+@pytest.mark.parametrize("F", [1, 7, 33, 20_003])
+def test_sgd_span_kernel_matches_general(ce, F):
+    """The contiguous-row SGD kernel (k_sgd_span260: D = ld = 260, K = C = 4)
+    against the general 8-lane kernel, reached through a padded view (ld =
+    264): the same FMA chains, so the same bits, ragged frame counts included."""
+    from conftest import fitted_members
+
+    _, sgd, Xt = fitted_members(n_test=F)
+    Xd = dev(Xt)
+    Xpad = torch.zeros((F, 264), dtype=torch.float64, device="cuda")
+    Xpad[:, :260] = Xd
+    got = ce.ops.sgd_predict_proba(Xd, sgd.coef_, sgd.intercept_).cpu().numpy()
+    want = ce.ops.sgd_predict_proba(Xpad[:, :260], sgd.coef_, sgd.intercept_).cpu().numpy()
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
 def test_frames_inference_to_selection(ce):
     """amg_test.py:426-445 with every step on the device: member inference over
     frames (GNB, SGD), per-song segment mean, stack with a song-level member,
