@@ -297,9 +297,8 @@ __global__ __launch_bounds__(256) void k_sgd_span260(SgdArgs a) {
     const f64x2* X2 = reinterpret_cast<const f64x2*>(a.X);
     const int64_t step = (int64_t)gridDim.x * 32;
     double* xw = xs[w];
-    f64x2 buf[NCH];
-    int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 8;
-    auto fetch = [&](int64_t fb) {
+    auto fetch = [&](f64x2(&buf)[NCH], int64_t fb) {
+        if (fb >= a.F) return;
         const int64_t c0 = fb * (D / 2);
 #pragma unroll
         for (int k = 0; k < NCH; ++k) {
@@ -307,8 +306,12 @@ __global__ __launch_bounds__(256) void k_sgd_span260(SgdArgs a) {
             if (c < SPAN && c0 + c < nchunks) buf[k] = __builtin_nontemporal_load(X2 + c0 + c);
         }
     };
-    if (f0 < a.F) fetch(f0);
-    for (; f0 < a.F; f0 += step) {
+    // one span: registers -> LDS slot, refill the registers one span ahead,
+    // then the classes' FMA chains (m outer: one x value live at a time)
+    auto span = [&](f64x2(&buf)[NCH], int64_t fc) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the previous span's reads precede these writes
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int k = 0; k < NCH; ++k) {
             const int c = k * 64 + lane;
@@ -320,24 +323,27 @@ __global__ __launch_bounds__(256) void k_sgd_span260(SgdArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double x[NX];
+        fetch(buf, fc + step);
+        double d[KC];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) x[m] = (m < NX - 1 || j < D - 8 * (NX - 1)) ? xw[g * RP + 8 * m + j] : 0.0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // every lane's reads precede the next span's writes
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (f0 + step < a.F) fetch(f0 + step);
+        for (int c = 0; c < KC; ++c) d[c] = 0.0;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) {
+            if (m < NX - 1 || j < D - 8 * (NX - 1)) {
+                const double x = xw[g * RP + 8 * m + j];
+#pragma unroll
+                for (int c = 0; c < KC; ++c) d[c] = fma(x, cf[c * D + 8 * m + j], d[c]);
+            }
+        }
         double p[KC > 1 ? KC : 2];
 #pragma unroll
-        for (int c = 0; c < KC; ++c) {
-            double d = 0.0;
-#pragma unroll
-            for (int m = 0; m < NX; ++m)
-                if (m < NX - 1 || j < D - 8 * (NX - 1)) d = fma(x[m], cf[c * D + 8 * m + j], d);
-            p[c] = sgd_expit(d, a.intercept[c]);
-        }
-        sgd_store(a, p, KC, f0 + g, j);
-    }
+        for (int c = 0; c < KC; ++c) p[c] = sgd_expit(d[c], a.intercept[c]);
+        sgd_store(a, p, KC, fc + g, j);
+    };
+    f64x2 b0[NCH];
+    int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 8;
+    fetch(b0, f0);
+    for (; f0 < a.F; f0 += step) span(b0, f0);
 }
 
 }  // namespace ce
