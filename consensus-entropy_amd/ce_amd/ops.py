@@ -82,6 +82,18 @@ def committee_entropy(P, layout="MNC", return_mean=False):
     return (ent, mean) if return_mean else ent
 
 
+def log_f64(x):
+    """glibc's log(x) as the engine evaluates it inside every entropy
+    (ce_log_f64; verification against the C library)."""
+    _on_gpu(x, "x")
+    x = x.contiguous()
+    if x.dtype != torch.float64:
+        raise ValueError("log_f64 takes float64")
+    y = torch.empty_like(x)
+    call("ce_log_f64", _p(x), x.numel(), _p(y), _stream(x.device))
+    return y
+
+
 def vote_table(votes, C=4):
     """amg_test.py:109-117 on int8 votes [N, A] (-1 = missing): (freq [N, C], ent [N])."""
     _on_gpu(votes, "votes")

@@ -1,8 +1,8 @@
 // ce_device.hpp -- device-side arithmetic of the selection path (gfx950).
 //
 // Every routine here restates one piece of the reference's NumPy/SciPy arithmetic
-// in f64, in the same operation order, so that the GPU path reproduces the
-// reference bit for bit wherever the C library's log and the device log agree
+// in f64, in the same operation order, with glibc's log restated
+// (ce_glibc_log.hpp), so that the GPU path reproduces the reference bit for bit
 // (see DESIGN.md "Numerics"):
 //   mean      np.mean(np.array(pred_prob), axis=0)        amg_test.py:441
 //   entropy   scipy.stats.entropy(consensus, axis=1)      amg_test.py:443,451,479
@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "ce_glibc_log.hpp"
 
 namespace ce {
 
@@ -39,9 +41,10 @@ __device__ __forceinline__ bool better(uint64_t ka, int64_t ia, uint64_t kb, int
 
 // scipy.special.entr: NaN -> NaN, x > 0 -> -x*log(x), x == 0 -> 0, x < 0 -> -inf.
 // Branch-free form: for x == 0 and x < 0 the product is replaced, so the
-// log of a non-positive argument never reaches the result.
+// log of a non-positive argument never reaches the result.  log is glibc's
+// (ce_glibc_log.hpp): the calling kernel has run stage_log_table().
 __device__ __forceinline__ double entr(double x) {
-    double r = -x * log(x);
+    double r = -x * dlog(x);
     r = (x == 0.0) ? 0.0 : r;
     r = (x < 0.0) ? -__builtin_inf() : r;
     return r;  // NaN input: x==0 and x<0 are false, r = -NaN*log(NaN) = NaN

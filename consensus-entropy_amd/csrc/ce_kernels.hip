@@ -138,6 +138,7 @@ __device__ __forceinline__ void write_list(const TopQSmem<CAP>& s, int cnt, int 
 template <class Src, int CAP, bool FINAL>
 __global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, Cand* __restrict__ wc, double* __restrict__ oval,
                                                  int64_t* __restrict__ oidx) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ TopQSmem<CAP> sm;
     TopQ<CAP, kBS> tq(sm);
     tq.init();
@@ -182,6 +183,7 @@ __device__ __forceinline__ double wide_item(const WideArgs& a, const PwPlan& pl,
 template <int DT, int NPL, bool VEC, int CAP, bool FINAL>
 __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q, Cand* __restrict__ wc,
                                                       double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ TopQSmem<CAP> sm;
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     TopQ<CAP, kBS> tq(sm);
@@ -213,6 +215,7 @@ __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg
 template <int DT, int NPL, bool VEC>
 __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                      Cand* __restrict__ wc) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ WaveLists sm;
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -249,6 +252,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 template <int DT, int KCH, int UNR>
 __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ WaveLists sm;
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
@@ -319,6 +323,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
 
 template <int DT, int NPL, bool VEC>
 __global__ __launch_bounds__(kBS) void k_wide_entropy_v(WideArgs a, PwPlan pl, double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     const int w = threadIdx.x >> 6;
     double* row = wsm + w * wide_lds_doubles(a.C);
@@ -625,6 +630,7 @@ __global__ __launch_bounds__(256) void k_merge_wave(ListSrc<FROM_VALS> src, int 
 template <class Src>
 __global__ __launch_bounds__(kBS) void k_entropy(Src src, int64_t N, double* __restrict__ mean_out,
                                                  double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     constexpr int C = Src::kC;
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBS) {
         double mean[C];
@@ -634,6 +640,12 @@ __global__ __launch_bounds__(kBS) void k_entropy(Src src, int64_t N, double* __r
             for (int c = 0; c < C; ++c) mean_out[i * C + c] = mean[c];
         ent[i] = entropy_row<C>(mean);
     }
+}
+
+// glibc log over a vector (verification of ce_glibc_log.hpp against libm).
+__global__ __launch_bounds__(kBS) void k_log(const double* __restrict__ x, int64_t n, double* __restrict__ y) {
+    stage_log_table();
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) y[i] = dlog(x[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -663,6 +675,7 @@ __device__ __forceinline__ void finish_counts(int (&cnt)[C], int64_t n_row, doub
 template <int C>
 __global__ __launch_bounds__(kBS) void k_vote(const int8_t* __restrict__ votes, int64_t N, int A, int64_t ld,
                                               double* __restrict__ freq, double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     const int lane = lane_id();
     for (int64_t n = (int64_t)blockIdx.x * (kBS / 64) + (threadIdx.x >> 6); n < N;
          n += (int64_t)gridDim.x * (kBS / 64)) {
@@ -681,6 +694,7 @@ __global__ __launch_bounds__(kBS) void k_vote(const int8_t* __restrict__ votes, 
 
 __global__ __launch_bounds__(kBS) void k_va(const double* __restrict__ va, int64_t N, int A,
                                             double* __restrict__ freq, double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     const int lane = lane_id();
     for (int64_t n = (int64_t)blockIdx.x * (kBS / 64) + (threadIdx.x >> 6); n < N;
          n += (int64_t)gridDim.x * (kBS / 64)) {
@@ -1186,6 +1200,21 @@ extern "C" int ce_committee_entropy(const void* p, ce_dtype dt, int64_t N, int32
     }
     if (rc) return dispatch_err(rc, a);
     return check_launch("ce_committee_entropy");
+}
+
+extern "C" int ce_log_f64(const double* x, int64_t n, double* y, ce_stream_t stream) {
+    if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad log arguments");
+    if (n == 0) return CE_OK;
+    const int grid = (int)std::min<int64_t>(cdiv(n, kBS), 8192);
+    hipLaunchKernelGGL(k_log, dim3(grid), dim3(kBS), 0, (hipStream_t)stream, x, n, y);
+    return check_launch("ce_log_f64");
+}
+
+extern "C" int ce_log_f64_host(const double* x, int64_t n, double* y) {
+    if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad log arguments");
+    const LogEntry* tab = host_log_table();
+    for (int64_t i = 0; i < n; ++i) y[i] = glibc_log(x[i], tab);
+    return CE_OK;
 }
 
 extern "C" int ce_vote_entropy(const int8_t* votes, int64_t N, int32_t A, int32_t C, int64_t ld,

@@ -386,6 +386,7 @@ __device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L
 // Item-major, dense rows of 16*S bytes, LDS-DMA staged (AUX: DMA cache policy).
 template <int DT, int C, int S, int AUX>
 __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* __restrict__ wc) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
@@ -445,6 +446,7 @@ __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, 
 
 template <class Src, int IPL, int UNR>
 __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, int q, Cand* __restrict__ wc) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ WaveLists sm;
     const int w = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
@@ -472,6 +474,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_
                                                             int64_t base_idx, int q, int bpu,
                                                             double* __restrict__ oval, int64_t* __restrict__ oidx,
                                                             Cand* __restrict__ wc, const uint32_t* __restrict__ excl) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ WaveListsT<WAVES> sm;
     __shared__ uint64_t fk_s[4 * WAVES];
     __shared__ int64_t fi_s[4 * WAVES];

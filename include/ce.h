@@ -151,6 +151,17 @@ size_t ce_xgb_lds_bytes(int32_t D, int32_t G);
 int ce_xgb_expf(const float *x, int64_t n, float *y, ce_stream_t stream);
 
 /*
+ * glibc's f64 log as the engine evaluates it inside every entropy
+ * (scipy.special.entr's log, amg_test.py:443; csrc/ce_glibc_log.hpp), exposed
+ * for verification against the C library:
+ *   ce_log_f64       y[i] = log(x[i]) on the device (x, y device memory)
+ *   ce_log_f64_host  the same restatement on the host CPU (x, y HOST memory;
+ *                    synchronous, no GPU needed)
+ */
+int ce_log_f64(const double *x, int64_t n, double *y, ce_stream_t stream);
+int ce_log_f64_host(const double *x, int64_t n, double *y);
+
+/*
  * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]
  * (amg_test.py:445, :452, :480).  Positions are reported as base_idx + i.
  * val_out: [q] f64, idx_out: [q] int64.

@@ -374,3 +374,20 @@ int64_t ce_ref_expf_check(const float *got, uint32_t start, int64_t count) {
     }
     return bad;
 }
+
+/* -------------------------------------------------------------------------
+ * The C library's log is what scipy.special.entr calls (amg_test.py:443 via
+ * scipy.stats.entropy).  got[i] = an implementation's log(x[i]): how many
+ * differ from libm's log bit for bit (NaN matches any NaN).
+ * ------------------------------------------------------------------------- */
+int64_t ce_ref_log_check(const double *x, const double *got, int64_t n) {
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double ref = log(x[i]);
+        uint64_t a, b;
+        memcpy(&a, &ref, 8);
+        memcpy(&b, &got[i], 8);
+        if (isnan(ref) ? !isnan(got[i]) : a != b) ++bad;
+    }
+    return bad;
+}

@@ -448,3 +448,38 @@ def oracle_expf_check(got, start):
     L.ce_ref_expf_check.restype = ctypes.c_int64
     L.ce_ref_expf_check.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64]
     return int(L.ce_ref_expf_check(_ptr(got), start, got.size))
+
+
+def oracle_log_check(x, got):
+    """Mismatches (bit for bit, NaN == NaN) between got and libm's log(x) --
+    the log scipy.special.entr calls (amg_test.py:443)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    got = np.ascontiguousarray(got, dtype=np.float64)
+    assert x.shape == got.shape
+    L = lib()
+    L.ce_ref_log_check.restype = ctypes.c_int64
+    L.ce_ref_log_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    return int(L.ce_ref_log_check(_ptr(x), _ptr(got), x.size))
+
+
+def log_test_arguments(n, seed):
+    """n f64 arguments covering every branch of glibc's log: uniform (0, 1)
+    (entropy terms), [0.5, 1) bit patterns, the near-1 window [1-2^-4,
+    1+0x1.09p-4), subnormals, all positive bit patterns, the values 1, 0, -0,
+    inf, NaN, negatives, and every table boundary z = 0x1.6p-1 * (1 + i/128)."""
+    rng = np.random.default_rng(seed)
+    k = n // 6
+    parts = [
+        rng.random(k),
+        (np.uint64(0x3FE0000000000000) + (rng.integers(0, 1 << 52, k, dtype=np.uint64))).view(np.float64),
+        1.0 - 2.0 ** -4 + rng.random(k) * (2.0 ** -4 + float.fromhex("0x1.09p-4")),
+        (rng.integers(1, 1 << 52, k, dtype=np.uint64)).view(np.float64),
+        (rng.integers(1, 0x7FF0000000000000, k, dtype=np.uint64)).view(np.float64),
+    ]
+    edges = np.array([1.0, 0.0, -0.0, np.inf, np.nan, -1.0, -np.inf, 5e-324, 2.2250738585072014e-308,
+                      1.0 - 2.0 ** -4, 1.0 + float.fromhex("0x1.09p-4"), np.nextafter(1.0, 0), np.nextafter(1.0, 2)])
+    zb = (np.uint64(0x3FE6000000000000) + (np.arange(256, dtype=np.uint64) << np.uint64(44)))
+    bnd = np.concatenate([zb - np.uint64(1), zb, zb + np.uint64(1)]).view(np.float64)
+    rest = n - sum(len(p) for p in parts) - len(edges) - len(bnd)
+    parts += [edges, bnd, rng.random(max(rest, 0)) * 2.0 ** rng.integers(-1074, 1, max(rest, 0))]
+    return np.concatenate(parts)
