@@ -17,9 +17,14 @@ reference's on the shrunken pool (tests/test_gpu_parity.py::test_session_*).
 Modes (amg_test.py:425-489):
   mc    committee over the full pool [M, N, C] (or [N, M, C]), excluding queried items
   hc    the human-consensus table, fixed at construction, excluding queried rows
-  mix   both, ALIGNED pools (hc row r is mc item r, N_h == N): a pick through
-        either part removes the song from both, as :484 + :521-531 do by id;
-        positions in [0, 2N) index the row stack [mc; hc] like select_queries
+  mix   both.  The hc table keeps the reference's OWN row order (annotation
+        order, :359/:376), not the committee's (sorted s_id, :437), so the
+        lowest-position tie-break inside the hc segment of [mc; hc] (:477) is
+        the reference's; ``hc_to_mc[j]`` names the committee item of hc row j
+        (-1: the song is not in the committee's pool).  A pick through either
+        part removes the song from both, as :484 + :521-531 do by id.
+        Positions: i in [0, N) = committee item i, N + j = hc row j (the row
+        stack [mc; hc] of select_queries, over the full pools)
   rand  uniform among the remaining items with the caller's RandomState
         (legacy np.random.shuffle of the remaining positions, first q)
 """
@@ -33,7 +38,8 @@ from .select import MODES, _device, _hc_tensor, stack_committee
 
 
 class SelectionSession:
-    def __init__(self, queries, mode, n_items, *, hc=None, votes=None, rng=None, device=None, n_classes=4):
+    def __init__(self, queries, mode, n_items, *, hc=None, votes=None, hc_to_mc=None, rng=None, device=None,
+                 n_classes=4):
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}, got {mode!r}")
         self.q = int(queries)
@@ -46,12 +52,28 @@ class SelectionSession:
         self.H = None
         if mode in ("hc", "mix"):
             self.H = _hc_tensor(hc, votes, n_classes, self.dev).to(torch.float64).contiguous()
-            if mode == "mix" and self.H.shape[0] != self.N:
-                raise ValueError("mix sessions need aligned pools: hc rows == n_items")
             if mode == "hc":
                 self.N = self.H.shape[0]
         self.excl = ops.excl_bitmap(self.N, self.dev)
         self.n_selected = 0
+        if mode == "mix":
+            Nh = self.H.shape[0]
+            if hc_to_mc is None:
+                if Nh != self.N:
+                    raise ValueError("mix: pass hc_to_mc (committee item of each hc row) when the pools differ")
+                hc_to_mc = np.arange(Nh)
+            h2m = np.asarray(hc_to_mc, dtype=np.int64).reshape(-1)
+            if h2m.shape[0] != Nh or (h2m >= self.N).any() or (h2m < -1).any():
+                raise ValueError("hc_to_mc must give, per hc row, a committee item in [0, n_items) or -1")
+            valid = h2m[h2m >= 0]
+            if len(np.unique(valid)) != len(valid):
+                raise ValueError("hc_to_mc maps two hc rows to one committee item")
+            m2h = np.full(self.N, -1, np.int64)
+            m2h[valid] = np.flatnonzero(h2m >= 0)
+            self.h2m = torch.from_numpy(h2m).to(self.dev)
+            self.m2h = torch.from_numpy(m2h).to(self.dev)
+            self.Nh = Nh
+            self.excl_hc = ops.excl_bitmap(Nh, self.dev)
 
     @property
     def remaining(self):
@@ -64,8 +86,8 @@ class SelectionSession:
             raise ValueError(f"committee covers {n} items, the session's pool has {self.N}")
         return ops.select_mc(P, self.q, lay, excl=self.excl)
 
-    def _hc(self):
-        return ops.select_mc(self.H.unsqueeze(1), self.q, "NMC", excl=self.excl)
+    def _hc(self, excl=None):
+        return ops.select_mc(self.H.unsqueeze(1), self.q, "NMC", excl=self.excl if excl is None else excl)
 
     def select(self, committee=None, layout="MNC"):
         """One epoch: returns the q picked positions (np.int64; fewer when the
@@ -91,16 +113,22 @@ class SelectionSession:
             if committee is None:
                 raise ValueError("mix mode needs `committee`")
             vm, im = self._mc(committee, layout)
-            vh, ih = self._hc()
+            vh, ih = self._hc(self.excl_hc)
             ih = torch.where(ih >= 0, ih + self.N, ih)
             _, idx = ops.topq_merge(torch.cat([vm, vh]), torch.cat([im, ih]), q)
             # a song leaves both pools whichever part picked it (:484, :521-531)
-            song = torch.where(idx >= self.N, idx - self.N, idx)
+            is_hc = idx >= self.N
+            row = (idx - self.N).clamp(0, self.Nh - 1)
+            item = idx.clamp(0, self.N - 1)
+            song = torch.where(idx < 0, idx, torch.where(is_hc, self.h2m[row], idx))
+            hrow = torch.where(idx < 0, idx, torch.where(is_hc, row, self.m2h[item]))
             ops.mark_selected(self.excl, self.N, song)
+            ops.mark_selected(self.excl_hc, self.Nh, hrow)
         out = idx.cpu().numpy()
         out = out[out >= 0]
         if self.mode == "mix":
-            self.n_selected += len(np.unique(np.where(out >= self.N, out - self.N, out)))
+            # songs leaving the committee pool (an hc pick of a song outside it leaves only the table)
+            self.n_selected += len(np.unique(song.cpu().numpy()[song.cpu().numpy() >= 0]))
         else:
             self.n_selected += len(out)
         return out

@@ -483,6 +483,50 @@ def test_session_equals_shrinking_pools(ce, mode):
         [np.where(x >= N, x - N, x) for x in exp])))
 
 
+def test_session_mix_hc_in_own_row_order(ce):
+    """Session mix with the hc table in the reference's own row order
+    (annotation order, amg_test.py:359/:376) while the committee is in sorted
+    s_id order (:437): hc rows tie heavily, so the lowest-position rule inside
+    the hc segment of [mc; hc] (:477) must follow the TABLE's order.  The table
+    covers only part of the pool.  Compared with the reference's shrinking-pool
+    loop, where a pick through either segment drops the song from both pools
+    (:484, :521-531)."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(77)
+    N, Nh, q, epochs = 3000, 2400, 10, 8
+    h2m = rng.permutation(N)[:Nh]                       # hc row j is committee item h2m[j]
+    m2h = np.full(N, -1)
+    m2h[h2m] = np.arange(Nh)
+    committees = [np.floor(synth(rng, N, 4, 4, np.float64) * 8).transpose(1, 0, 2) / 8 + 1e-3
+                  for _ in range(epochs)]
+    hc = np.round(rng.dirichlet(np.ones(4), Nh), 1)     # few distinct rows: ties everywhere
+    hc[::5] = [0.25, 0.25, 0.25, 0.25]                   # the maximal entropy, many times
+    alive, alive_h = np.ones(N, bool), np.ones(Nh, bool)
+    sess = ce.SelectionSession(q, "mix", N, hc=hc, hc_to_mc=h2m)
+    hc_picks = 0
+    for e in range(epochs):
+        pos, hpos = np.flatnonzero(alive), np.flatnonzero(alive_h)
+        ent = np.concatenate([O.oracle_committee_entropy(committees[e][:, pos], "MNC"),
+                              O.oracle_table_entropy(hc[hpos])])
+        _, i = O.oracle_topq(ent, q)
+        n = len(pos)
+        exp = np.where(i < n, pos[np.minimum(i, n - 1)], N + hpos[np.maximum(i - n, 0)])
+        got = sess.select(committee=dev(committees[e]))
+        assert np.array_equal(got, exp), (e, got, exp)
+        hc_picks += int((exp >= N).sum())
+        for p in exp:
+            if p < N:
+                alive[p] = False
+                if m2h[p] >= 0:
+                    alive_h[m2h[p]] = False
+            else:
+                alive_h[p - N] = False
+                alive[h2m[p - N]] = False
+    assert sess.remaining == alive.sum()
+    assert hc_picks > 0  # the hc segment took part
+
+
 def test_session_rand_and_exhaustion(ce):
     """rand draws only remaining items; a pool smaller than q*epochs runs dry
     without repeats; the exclusion API rejects q > 64."""
