@@ -162,6 +162,8 @@ def select_queries(mode, q, *, committee=None, hc=None, votes=None, pool=None, r
     q = int(q)
     if q < 1:
         raise ValueError("q must be >= 1")
+    if q > ops._lib.CE_MAX_Q and mode != "rand":
+        raise ValueError(f"q = {q} exceeds the engine's CE_MAX_Q = {ops._lib.CE_MAX_Q} queries per call")
     if mode == "rand":
         if pool is None:
             raise ValueError("rand mode needs `pool`")
@@ -173,19 +175,19 @@ def select_queries(mode, q, *, committee=None, hc=None, votes=None, pool=None, r
         if committee is None:
             raise ValueError("mc mode needs `committee`")
         P, lay = stack_committee(committee, dev, layout)
-        _, idx = ops.select_mc(P, min(q, ops._lib.CE_MAX_Q), lay)
+        _, idx = ops.select_mc(P, q, lay)
         return _positions(idx)
     if mode == "hc":
         H = _hc_tensor(hc, votes, n_classes, dev)
         P = H.unsqueeze(1)  # [N_h, M=1, C]: mean over one member is the row itself
-        _, idx = ops.select_mc(P, min(q, ops._lib.CE_MAX_Q), "NMC")
+        _, idx = ops.select_mc(P, q, "NMC")
         return _positions(idx)
     # mix
     if committee is None:
         raise ValueError("mix mode needs `committee`")
     P, lay = stack_committee(committee, dev, layout)
     H = _hc_tensor(hc, votes, n_classes, dev)
-    _, idx = ops.select_mix(P, H, min(q, ops._lib.CE_MAX_Q), lay)
+    _, idx = ops.select_mix(P, H, q, lay)
     return _positions(idx)
 
 
@@ -213,7 +215,7 @@ class ConsensusEntropySelector:
         if mode == "rand":
             return select_queries("rand", q, pool=pool_ids, rng=self.rng), consensus_hc
         if mode in ("mc", "mix"):
-            if not pred_prob:
+            if pred_prob is None or len(pred_prob) == 0:
                 raise ValueError(f"{mode} mode needs pred_prob")
             last_index = list(getattr(pred_prob[-1], "index", range(len(pred_prob[-1]))))
         if mode == "mc":

@@ -70,8 +70,11 @@ class XgbForest:
         lrn = model["learner"]
         mp = lrn["learner_model_param"]
         objective = lrn.get("objective", {}).get("name", "multi:softprob")
-        if objective not in ("multi:softprob", "multi:softmax", "binary:logistic"):
-            raise ValueError(f"objective {objective!r} is not a classifier predict_proba path")
+        if objective not in ("multi:softprob", "binary:logistic"):
+            # multi:softmax's booster output is the class label; XGBClassifier.predict_proba
+            # then returns [1 - label, label] (xgboost/sklearn.py:1025-1029), not probabilities
+            raise ValueError(f"objective {objective!r} has no probability output (multi:softprob or "
+                             "binary:logistic only)")
         gb = lrn["gradient_booster"]
         if gb.get("name", "gbtree") != "gbtree":
             raise ValueError(f"booster {gb.get('name')!r} unsupported (gbtree only)")

@@ -176,6 +176,37 @@ __host__ __device__ __forceinline__ double glibc_log(double x, const LogEntry* t
     return y + hi;
 }
 
+// The same function, laid out for the device: the common case (x outside the
+// near-1 window, positive, normal, finite -- every entropy term p of a row
+// with more than one non-negligible class) is straight-line 32-bit integer +
+// f64 FMA code; the near-1 window and the special inputs take glibc_log()
+// above under a branch the whole wave usually skips.  Same bits as glibc_log
+// for every input (the common-case operations are glibc_log's own).
+__host__ __device__ __forceinline__ double glibc_log_fast(double x, const LogEntry* tab) {
+    constexpr double A[5] = {CE_GLIBC_LOG_A};
+    constexpr double Ln2[2] = {CE_GLIBC_LOG_LN2};
+    const uint64_t ix = dbits(x);
+    const uint32_t hw = (uint32_t)(ix >> 32);
+    const uint32_t thi = hw - 0x3fe60000u;                    // high word of ix - OFF (OFF's low word is 0)
+    const int i = (int)((thi >> 13) & 127u);                  // (tmp >> 45) % 128
+    const int k = (int)thi >> 20;                             // (int64_t)tmp >> 52
+    const uint32_t izh = hw - (thi & 0xfff00000u);            // ix - (tmp & 0xfff << 52)
+    const double z = bitsd(((uint64_t)izh << 32) | (uint32_t)ix);
+    const LogEntry e = tab[i];
+    const double r = __builtin_fma(z, e.invc, -1.0);
+    const double kd = (double)k;
+    const double w = __builtin_fma(kd, Ln2[0], e.logc);
+    const double hi = w + r;
+    const double lo = __builtin_fma(kd, Ln2[1], w - hi + r);
+    const double r2 = r * r;
+    const double p = __builtin_fma(r2, __builtin_fma(r, A[4], A[3]), __builtin_fma(r, A[2], A[1]));
+    const double y = __builtin_fma(r * r2, p, __builtin_fma(r2, A[0], lo)) + hi;
+    const bool near1 = ix - 0x3fee000000000000ull < 0x3ff1090000000000ull - 0x3fee000000000000ull;
+    const bool special = (hw >> 16) - 0x0010u >= 0x7ff0u - 0x0010u;
+    if (__builtin_expect(near1 || special, 0)) return glibc_log(x, tab);
+    return y;
+}
+
 // The block's LDS copy of the table (every kernel that computes an entropy
 // calls stage_log_table() at its top, before any early exit).
 __shared__ __attribute__((aligned(16))) LogEntry s_log_tab[128];
@@ -186,7 +217,24 @@ __device__ __forceinline__ const LogEntry* stage_log_table() {
     __syncthreads();
     return s_log_tab;
 }
-__device__ __forceinline__ double dlog(double x) { return glibc_log(x, s_log_tab); }
+__device__ __forceinline__ double dlog(double x) { return glibc_log_fast(x, s_log_tab); }
+
+// Split staging for latency-bound kernels: fetch() issues the table loads at
+// kernel start (before the data loads), commit() -- once the data has been
+// waited for anyway -- writes them to LDS and syncs the block (block-uniform).
+// Needs blockDim.x >= 128.
+struct LogTablePrefetch {
+    double invc, logc;
+    __device__ __forceinline__ void fetch() {
+        const int j = threadIdx.x < 128 ? threadIdx.x : 127;
+        invc = g_log_tab[2 * j];
+        logc = g_log_tab[2 * j + 1];
+    }
+    __device__ __forceinline__ void commit() const {
+        if (threadIdx.x < 128) s_log_tab[threadIdx.x] = LogEntry{invc, logc};
+        __syncthreads();
+    }
+};
 
 inline const LogEntry* host_log_table() { return reinterpret_cast<const LogEntry*>(h_log_tab); }
 

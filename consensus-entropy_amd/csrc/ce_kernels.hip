@@ -40,6 +40,10 @@ constexpr int kSegWaves = 16;     // waves per single-block pool / per user (k_s
 // ---------------------------------------------------------------------------
 // Item sources.  key(i) returns the order key of global item i.
 // ---------------------------------------------------------------------------
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
 template <int DT, int C, bool VEC>
 struct CommitteeSrc {
     const void* p;
@@ -54,15 +58,58 @@ struct CommitteeSrc {
         committee_mean<DT, C, VEC, kUnr>(p, i * sN, M, sM, sC, dM, invM, pow2, m);
     }
     // IPL items at once: all their member loads in flight together
-    template <int UNR, int IPL>
-    __device__ __forceinline__ void keys(const int64_t (&items)[IPL], uint64_t (&k)[IPL]) const {
+    // hook() runs after the means, before the first log (e.g. LogTablePrefetch::commit)
+    template <int UNR, int IPL, class Hook = NoHook>
+    __device__ __forceinline__ void keys(const int64_t (&items)[IPL], uint64_t (&k)[IPL], Hook hook = {}) const {
         int64_t offs[IPL];
 #pragma unroll
         for (int u = 0; u < IPL; ++u) offs[u] = items[u] * sN;
         double m[IPL][C];
         committee_mean_multi<DT, C, VEC, UNR, IPL>(p, offs, M, sM, sC, dM, invM, pow2, m);
+        hook();
 #pragma unroll
         for (int u = 0; u < IPL; ++u) k[u] = order_key(entropy_row<C>(m[u]));
+    }
+    // keys() for latency-bound single-block pools: when the whole committee
+    // fits one batch (M <= UNR) the loads are issued item by item and each
+    // item's mean + entropy runs as soon as ITS loads have landed, so only the
+    // last item's arithmetic trails the last load.  Items u >= nlive (wave-
+    // uniform: no lane of the wave owns a real item there) skip the arithmetic
+    // (key 0).  hook() as in keys().
+    template <int UNR, int IPL, class Hook = NoHook>
+    __device__ __forceinline__ void keys_small(const int64_t (&items)[IPL], uint64_t (&k)[IPL], int nlive,
+                                               Hook hook = {}) const {
+        if (M > UNR) {
+            keys<UNR, IPL>(items, k, hook);
+            return;
+        }
+        MemberLoad<DT, C, VEC> ld[IPL][UNR];
+#pragma unroll
+        for (int u = 0; u < IPL; ++u)
+#pragma unroll
+            for (int v = 0; v < UNR; ++v) ld[u][v].load(p, items[u] * sN + (int64_t)(v < M ? v : M - 1) * sM, sC);
+        hook();
+        auto item = [&](auto full) {
+#pragma unroll
+            for (int u = 0; u < IPL; ++u) {
+                k[u] = 0;
+                if (u >= nlive) continue;  // wave-uniform
+                double acc[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) acc[c] = 0.0;
+#pragma unroll
+                for (int v = 0; v < UNR; ++v) {
+                    if constexpr (decltype(full)::value) ld[u][v].add_to(acc);  // M == UNR: no padding
+                    else ld[u][v].add_masked(acc, v < M);
+                }
+                double m[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) m[c] = div_members(acc[c], dM, invM, pow2);
+                k[u] = order_key(entropy_row<C>(m));
+            }
+        };
+        if (M == UNR) item(std::true_type());
+        else item(std::false_type());
     }
     __device__ __forceinline__ double entropy(int64_t i) const {
         double m[C];
@@ -1044,6 +1091,29 @@ static void with_seg_batching(F&& f) {
     else f(std::integral_constant<int, 4>(), std::integral_constant<int, 2>());
 }
 
+// Single-block pools (k_select_small): IPT items per thread (2 for C = 8
+// rows), UNR member loads per item in flight (f64 / C = 8 rows are twice as
+// wide: 2).  Returns false (nothing launched) when the pool exceeds BS * IPT.
+constexpr int kSmallBS = 512;       // batched users: 2 blocks per CU, all 500 users resident
+constexpr int kSmallBSWide = 1024;  // one pool of up to 4096 items
+template <class Src>
+constexpr int small_ipt() { return Src::kC > 4 ? 2 : 4; }
+template <class Src, int BS>
+static void launch_small(const Src& src, int grid, const int64_t* offsets, int64_t n, int64_t base_idx, int q,
+                         double* oval, int64_t* oidx, const uint32_t* excl, hipStream_t st) {
+    constexpr int UNR = (Src::kDT == kF64 || Src::kC > 4 || BS > kSmallBS) ? 2 : 4;
+    hipLaunchKernelGGL((k_select_small<Src, small_ipt<Src>(), UNR, BS>), dim3((unsigned)grid), dim3(BS), 0, st, src,
+                       offsets, n, base_idx, q, oval, oidx, excl);
+}
+static bool small_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("CE_AMD_SMALL");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 // Blocks of `kernel` resident on the whole device (occupancy API x CUs), cached.
 static int device_cus() {
     static int cus[64] = {0};
@@ -1202,6 +1272,12 @@ extern "C" int ce_committee_entropy(const void* p, ce_dtype dt, int64_t N, int32
     return check_launch("ce_committee_entropy");
 }
 
+#ifdef CE_PHASE_TIMING
+extern "C" int ce_debug_phase(uint64_t* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), (size_t)n * 6 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int ce_log_f64(const double* x, int64_t n, double* y, ce_stream_t stream) {
     if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad log arguments");
     if (n == 0) return CE_OK;
@@ -1213,7 +1289,7 @@ extern "C" int ce_log_f64(const double* x, int64_t n, double* y, ce_stream_t str
 extern "C" int ce_log_f64_host(const double* x, int64_t n, double* y) {
     if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad log arguments");
     const LogEntry* tab = host_log_table();
-    for (int64_t i = 0; i < n; ++i) y[i] = glibc_log(x[i], tab);
+    for (int64_t i = 0; i < n; ++i) y[i] = glibc_log_fast(x[i], tab);
     return CE_OK;
 }
 
@@ -1302,6 +1378,9 @@ extern "C" int ce_gnb_predict_proba(const double* X, int64_t F, int32_t D, int64
     if (F < 0 || D < 1 || D > kMaxFeat || ld < D || C < 1 || C > kMaxMemberC || ld_out < C)
         return fail(CE_EINVAL, "bad GaussianNB shapes F=%lld D=%d C=%d", (long long)F, D, C);
     if ((F > 0 && (!X || !out)) || !theta || !var || !log_prior) return fail(CE_EINVAL, "null pointer");
+    // numpy sums fewer than 8 features sequentially; the 8-lane pairwise kernel
+    // has no leaf for them (the reference's members have 260 features)
+    if (D < 8) return fail(CE_EUNSUPPORTED, "GaussianNB needs D >= 8 features (got %d)", D);
     if (F == 0) return CE_OK;
     GnbArgs a{X, F, D, ld, theta, var, log_prior, C, out, ld_out};
     const PwPlan pl = pw_plan(D);
@@ -1433,6 +1512,21 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
     if (rc0) return rc0;
     // the workspace contract holds on every path, even the one that does not touch it
     if (!ws || ws_bytes < lists_bytes(pool_blocks(N), q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (small_enabled() && q <= kStreamMaxQ && N > 0) {
+        // one block scores and selects the whole pool (k_select_small)
+        bool launched = false;
+        const int rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            if (N <= (int64_t)kSmallBS * small_ipt<S>()) {
+                launch_small<S, kSmallBS>(src, 1, nullptr, N, base_idx, q, val_out, idx_out, excl, st);
+                launched = true;
+            } else if (N <= (int64_t)kSmallBSWide * small_ipt<S>()) {
+                launch_small<S, kSmallBSWide>(src, 1, nullptr, N, base_idx, q, val_out, idx_out, excl, st);
+                launched = true;
+            }
+        });
+        if (rc == CE_OK && launched) return check_launch("ce_select_mc");
+    }
     if (stream_enabled() && q <= kStreamMaxQ && N > 0 &&
         N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes) {
         // small pool: ~512 items per 4-wave block on a few CUs (one block: it
@@ -1594,6 +1688,19 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     if (!ws || ws_bytes < lists_bytes(nl, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, nl, q);
+    if (small_enabled() && q <= kStreamMaxQ) {
+        // one 512-thread block per user when the average user fits one sweep
+        // (k_select_small; a longer user streams inside its block)
+        bool launched = false;
+        rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            if (cdiv(total_items, U) <= (int64_t)kSmallBS * small_ipt<S>()) {
+                launch_small<S, kSmallBS>(src, U, offsets, 0, 0, q, val_out, idx_out, nullptr, st);
+                launched = true;
+            }
+        });
+        if (rc == CE_OK && launched) return check_launch("ce_select_batched");
+    }
     if (stream_enabled() && q <= kStreamMaxQ) {
         // bpu 4-wave blocks per user, then one wave per user merges its bpu lists
         rc = with_committee(a, [&](auto src) {

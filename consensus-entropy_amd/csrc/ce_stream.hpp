@@ -563,5 +563,206 @@ __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Small pools in ONE block each (the per-user loop of amg_test.py:345 around
+// :441-445 in one launch; also a single pool of <= BS*IPT items): no second
+// launch, no per-wave lists, no tree merge, no sort network.
+//   1. the log table's loads are issued, then ALL member loads of the
+//      thread's IPT items (item tid + BS*v: each wave's loads coalesced); the
+//      table reaches LDS while the data is awaited anyway;
+//   2. the best key of each group of BS/64 lanes (lane-exchange butterfly) ->
+//      64 group bests (distinct items) in LDS; every thread ranks one of them
+//      against a 1/W slice of the others, and the group best of rank q-1 is
+//      the floor: q items are >= it, so only items >= the floor can be
+//      selected (exact);
+//   3. items >= the floor are appended to an LDS list (one atomic per wave);
+//      survivor t (usually ~q of them) counts the survivors that beat it and
+//      writes itself to output slot `rank` if rank < q.
+// A pool longer than BS*IPT, or more than CAP survivors (masses of exact ties
+// at the floor), takes per-wave register lists + a tree merge instead
+// (block-uniform branches, same answer).
+// offsets == nullptr: one pool [0, n) with positions base_idx + i; else block u
+// is user u, positions user-local.  excl: exclusion bitmap, or nullptr.
+// ---------------------------------------------------------------------------
+template <int GS>
+__device__ __forceinline__ void group_best(uint64_t& k, int64_t& i) {
+    uint64_t pk;
+    int64_t pi;
+#define CE_GB(J)                    \
+    if constexpr (GS > J) {         \
+        pk = k;                     \
+        pi = i;                     \
+        xor_cand<J>(pk, pi);        \
+        if (better(pk, pi, k, i)) { \
+            k = pk;                 \
+            i = pi;                 \
+        }                           \
+    }
+    CE_GB(1) CE_GB(2) CE_GB(4) CE_GB(8)
+#undef CE_GB
+}
+
+#ifdef CE_PHASE_TIMING
+// diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
+__device__ uint64_t g_phase[4096][6];
+#define CE_STAMP(b, k) \
+    if (threadIdx.x == 0 && (b) < 4096) g_phase[b][k] = wall_clock64();
+#else
+#define CE_STAMP(b, k)
+#endif
+
+template <int WAVES>
+struct SmallSmem {
+    static constexpr int CAP = 64 * WAVES;  // one survivor per thread
+    uint64_t gk[64];                        // group bests
+    int64_t gi[64];
+    int part[WAVES][64];                    // partial ranks of the group bests
+    int cnt;                                // survivors appended
+    uint64_t ck[CAP];
+    int64_t ci[CAP];
+    WaveListsT<WAVES> lists;                // fallback tree merge
+};
+
+template <class Src, int IPT, int UNR, int BS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_select_small(
+    Src src, const int64_t* __restrict__ offsets, int64_t n, int64_t base_idx, int q, double* __restrict__ oval,
+    int64_t* __restrict__ oidx, const uint32_t* __restrict__ excl) {
+    constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
+    static_assert(BS % 64 == 0 && BS >= 128 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
+    using SM = SmallSmem<W>;
+    __shared__ SM sm;
+    CE_STAMP(blockIdx.x, 0)
+    LogTablePrefetch tab;
+    tab.fetch();
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int u = blockIdx.x;
+    const int64_t s0 = offsets ? offsets[u] : 0, s1 = offsets ? offsets[u + 1] : n;
+    const int64_t len = s1 > s0 ? s1 - s0 : 0;
+    const int64_t rel = (offsets ? 0 : base_idx) - s0;  // position = item + rel
+    double* ov = oval + (int64_t)u * q;
+    int64_t* oi = oidx + (int64_t)u * q;
+    if (len > (int64_t)BS * IPT) {  // long pool: per-wave streams + tree merge (block-uniform)
+        tab.commit();
+        constexpr int64_t kIt = 64 * 2;
+        const int64_t its = (len + kIt - 1) / kIt, its_w = (its + W - 1) / W;
+        int64_t lo = s0 + (int64_t)w * its_w * kIt;
+        int64_t hi = lo + its_w * kIt < s1 ? lo + its_w * kIt : s1;
+        if (lo > hi) lo = hi;
+        RegTopQ tq;
+        tq.init(q);
+        stream_direct_range<Src, 2, UNR>(src, lo, hi, rel, q, tq, excl);
+        block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
+        return;
+    }
+    // 1. keys of this thread's IPT items, every load in flight before any math
+    int64_t items[IPT];
+    uint64_t k[IPT];
+    bool ok[IPT];
+#pragma unroll
+    for (int v = 0; v < IPT; ++v) {
+        const int64_t j = tid + (int64_t)BS * v;
+        items[v] = s0 + (j < len ? j : (len > 0 ? len - 1 : 0));
+        k[v] = 0;
+    }
+    int nlive = 0;  // this wave's item slots holding at least one real item (a prefix)
+#pragma unroll
+    for (int v = 0; v < IPT; ++v) nlive += (int64_t)BS * v + 64 * w < len;
+    if (len > 0) {  // block-uniform
+        src.template keys_small<UNR, IPT>(items, k, nlive, [&]() { tab.commit(); });
+    } else {
+        tab.commit();
+    }
+    CE_STAMP(u, 1)
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+#pragma unroll
+    for (int v = 0; v < IPT; ++v) {
+        ok[v] = tid + (int64_t)BS * v < len;
+        if (excl) ok[v] = ok[v] && !excluded(excl, items[v]);
+        if (ok[v] && better(k[v], items[v] + rel, bk, bi)) {
+            bk = k[v];
+            bi = items[v] + rel;
+        }
+    }
+    // 2. floor = the group best of rank q-1 (ranks split over the waves)
+    group_best<GS>(bk, bi);
+    if ((tid & (GS - 1)) == 0) {
+        sm.gk[tid / GS] = bk;
+        sm.gi[tid / GS] = bi;
+    }
+    if (tid == 0) sm.cnt = 0;
+    __syncthreads();
+    {
+        const uint64_t mk = sm.gk[lane];
+        const int64_t mi = sm.gi[lane];
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < 64 / W; ++j) {
+            const int o = w * (64 / W) + j;
+            r += better(sm.gk[o], sm.gi[o], mk, mi);
+        }
+        sm.part[w][lane] = r;
+    }
+    __syncthreads();
+    uint64_t fk = 0;  // no group best of rank q-1 (fewer valid groups): admit every valid item
+    int64_t fi = INT64_MAX;
+    {
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) r += sm.part[j][lane];
+        const uint64_t hit = __ballot(r == q - 1);
+        if (hit) {
+            const int sl = __builtin_ctzll(hit);
+            fk = sm.gk[sl];
+            fi = sm.gi[sl];
+        }
+    }
+    CE_STAMP(u, 2)
+    // 3. survivors (not worse than the floor) -> LDS list
+#pragma unroll
+    for (int v = 0; v < IPT; ++v) {
+        const int64_t pos = items[v] + rel;
+        const bool pass = ok[v] && !better(fk, fi, k[v], pos);
+        const uint64_t m = __ballot(pass);
+        if (m) {  // wave-uniform
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&sm.cnt, __popcll(m));
+            base = __builtin_amdgcn_readfirstlane(base);
+            const int slot =
+                base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (pass && slot < SM::CAP) {
+                sm.ck[slot] = k[v];
+                sm.ci[slot] = pos;
+            }
+        }
+    }
+    __syncthreads();
+    CE_STAMP(u, 3)
+    const int nc = sm.cnt;
+    if (nc <= SM::CAP) {
+        if (tid < nc) {  // survivor tid takes the output slot of its rank
+            const uint64_t mk = sm.ck[tid];
+            const int64_t mi = sm.ci[tid];
+            int r = 0;
+            for (int j = 0; j < nc; ++j) r += better(sm.ck[j], sm.ci[j], mk, mi);
+            if (r < q) {
+                ov[r] = key_to_val(mk);
+                oi[r] = mi;
+            }
+        } else if (tid < q) {  // fewer survivors than q: padding
+            ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
+            oi[tid] = -1;
+        }
+        CE_STAMP(u, 4)
+        return;
+    }
+    // overflow (> CAP items tie at or above the floor): per-wave lists + tree merge
+    RegTopQ tq;
+    tq.init(q, fk, fi == INT64_MAX ? fi : fi + 1);  // admit candidates >= the floor
+#pragma unroll
+    for (int v = 0; v < IPT; ++v) tq.offer(k[v], items[v] + rel, ok[v]);
+    block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
+}
+
 }  // namespace ce
 

@@ -11,7 +11,7 @@
 //     margin of its group tree_info[t]: preds[g] += leaf (float32, sequential);
 //   * a tree is walked from the root: missing feature -> the default child,
 //     else fvalue < split_cond ? left : right (RegTree::GetNext);
-//   * multi:softprob: Softmax over the row (first maximum; e_c = expf(m_c - max);
+//   * multi:softprob: Softmax over the row (fmaxf maximum; e_c = expf(m_c - max);
 //     wsum += e_c in float32 from 0; e_c /= wsum); binary:logistic:
 //     p = 1 / (1 + expf(-m)), returned as [1 - p, p] (sklearn.py:1027-1029).
 //   * expf is glibc's (>= 2.27, the x86-64 FMA ifunc variant): restated below
@@ -154,18 +154,16 @@ __device__ __forceinline__ void transform_store(const float* mg, int G, int C, i
         const float p1 = 1.0f / (1.0f + glibc_expf(-m));
         p[0] = 1.0f - p1;
         p[1] = p1;
-    } else {  // multi:softprob -> common::Softmax
+    } else {  // multi:softprob -> common::Softmax (xgboost src/common/math.h)
         float mx = mg[lane];
-        for (int g = 1; g < G; ++g) {
-            const float v = mg[g * 64 + lane];
-            if (v > mx) mx = v;
-        }
-        float wsum = 0.0f;
+        for (int g = 1; g < G; ++g) mx = fmaxf(mg[g * 64 + lane], mx);
+        double wsum = 0.0;  // xgboost: double wsum = 0.0f; ... *i /= static_cast<float>(wsum)
         for (int g = 0; g < G; ++g) {
             p[g] = glibc_expf(mg[g * 64 + lane] - mx);
             wsum += p[g];
         }
-        for (int g = 0; g < G; ++g) p[g] /= wsum;
+        const float ws = (float)wsum;
+        for (int g = 0; g < G; ++g) p[g] /= ws;
     }
     for (int c = 0; c < C; ++c) {
         if constexpr (ODT == CE_F64)
@@ -249,7 +247,7 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
     const int c = min(kXgbChunk, (n + S - 1) / S);
     const int head_end = max(k0, k1 - (S - 1) * c);
     float m = a.base;
-    uint32_t packed[kXgbChunk / 2];  // tail waves: leaf indices, 16 bits each
+    uint32_t packed[kXgbChunk / 2] = {};  // tail waves: leaf indices, 16 bits each
     int lo = 0, cnt = 0;
     if (s == 0) {
         float pend[8];
@@ -289,11 +287,14 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
             m = mg[g * 64 + lane];
 #pragma unroll
             for (int b = 0; b < kXgbChunk / 8; ++b) {
+                if (b * 8 >= cnt) break;  // wave-uniform; never load past the wave's trees
                 float v[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
+                    // slots past cnt hold the leaf of the batch's clamped last tree (leafidx8):
+                    // re-read that (tree, leaf) -- in bounds, not added
                     const int i = b * 8 + j;
-                    v[j] = fl.value(lo + (i < cnt ? i : 0), (packed[i / 2] >> (16 * (i & 1))) & 0xffffu);
+                    v[j] = fl.value(lo + min(i, cnt - 1), (packed[i / 2] >> (16 * (i & 1))) & 0xffffu);
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j)

@@ -109,7 +109,8 @@ int ce_segment_mean(const void *frames, ce_dtype dt, int64_t F, int32_t C, int64
  * predict_proba of the reference's linear members (amg_test.py:435, :467;
  * deam_classifier.py:211-218) over frames X [F, D] f64 (row stride ld),
  * written to out [F, C] f64 (row stride ld_out), e.g. the input of
- * ce_segment_mean.  D <= 512 features (the reference: 260), C <= 8 classes.
+ * ce_segment_mean.  D <= 512 features (the reference: 260; GaussianNB needs
+ * D >= 8, CE_EUNSUPPORTED below), C <= 8 classes.
  *   ce_gnb_predict_proba  GaussianNB (sklearn 0.24.1): theta / var [C, D]
  *                         (theta_, sigma_), log_prior [C] = log(class_prior_);
  *                         numpy's pairwise sums over features, scipy's logsumexp

@@ -262,8 +262,10 @@ int64_t ce_ref_topq_merge(const double *vals, const int64_t *idx, int64_t L, int
  *     walk from node 0 -- missing -> default child, else
  *     fvalue < split_cond ? left : right (RegTree::GetNext) -- until a leaf,
  *     then preds[row][tree_info[t]] += leaf (float32)  (PredictByAllTrees);
- *   - multi:softprob: common::Softmax (first max; expf(m - max); wsum float
- *     from 0; divide); binary:logistic: 1/(1+expf(-m)) -> [1-p, p].
+ *   - multi:softprob: common::Softmax (src/common/math.h: wmax = fmaxf over
+ *     the row; e = expf(m - wmax); `double wsum = 0.0f` accumulates the float
+ *     e's in double; each e /= static_cast<float>(wsum));
+ *     binary:logistic: 1/(1+expf(-m)) -> [1-p, p] (sklearn.py:1025-1029).
  * The trees are the model's own node arrays (xgboost JSON: left_children,
  * right_children, split_indices, split_conditions -- the leaf value at a leaf
  * --, default_left), tree t's nodes at [node_off[t], node_off[t+1]).
@@ -349,14 +351,14 @@ int ce_ref_xgb_predict_proba(const double *X, int64_t F, int32_t D, int64_t ld, 
             p[1] = p1;
         } else {
             float mx = preds[0];
-            for (int g = 1; g < G; ++g)
-                if (preds[g] > mx) mx = preds[g];
-            float wsum = 0.0f;
+            for (int g = 1; g < G; ++g) mx = fmaxf(preds[g], mx);
+            double wsum = 0.0; /* common::Softmax: double accumulator, one float cast */
             for (int g = 0; g < G; ++g) {
                 p[g] = ce_ref_expf(preds[g] - mx);
                 wsum += p[g];
             }
-            for (int g = 0; g < G; ++g) p[g] /= wsum;
+            const float ws = (float)wsum;
+            for (int g = 0; g < G; ++g) p[g] /= ws;
         }
     }
     return 0;

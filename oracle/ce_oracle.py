@@ -431,13 +431,12 @@ def ref_xgb_predict_proba_py(X, model):
         else:
             mx = preds[0]
             for v in preds[1:]:
-                if v > mx:
-                    mx = v
+                mx = np.float32(max(v, mx))  # fmaxf (margins are finite)
             e = [libm_expf(np.float32(v - mx)) for v in preds]
-            ws = np.float32(0.0)
+            ws = 0.0  # common::Softmax: `double wsum`; Python floats are IEEE doubles
             for v in e:
-                ws = np.float32(ws + v)
-            out[r] = [np.float32(v / ws) for v in e]
+                ws += float(v)
+            out[r] = [np.float32(v / np.float32(ws)) for v in e]
     return out
 
 

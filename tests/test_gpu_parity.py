@@ -317,6 +317,49 @@ def test_batched_segments_vs_oracle(ce, sizes):
         assert np.array_equal(got, io), u
 
 
+@pytest.mark.parametrize("q", [10, 1, 64])
+def test_batched_500_users_vs_oracle(ce, q):
+    """BASELINE configs[2] at its full size: 500 users x 4 members x 1608
+    excerpts x 4 classes fp32 in one launch (one block per user), every user's
+    top-q against the oracle; the committee is quantised so exact ties cross
+    the q-th boundary."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(500 + q)
+    U, Nu = 500, 1608
+    offs = np.arange(U + 1, dtype=np.int64) * Nu
+    P = synth(rng, U * Nu, 4, 4, np.float32, quant=32)
+    ent_o = O.oracle_committee_entropy(P, "NMC")
+    _, idx = ce.ops.select_batched(dev(np.ascontiguousarray(np.transpose(P, (1, 0, 2)))), dev(offs), q, "MNC")
+    idx = idx.cpu().numpy()
+    for u in range(U):
+        io = O.oracle_topq(ent_o[offs[u]:offs[u + 1]], q)[1]
+        assert np.array_equal(idx[u][idx[u] >= 0], io), u
+
+
+def test_batched_tie_floods(ce):
+    """Users whose items tie in masses at the floor (all-equal rows, two-valued
+    rows, NaN rows): the single-block survivor list overflows and the kernel
+    takes its per-wave fallback -- lowest positions first, NaN first."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(12)
+    sizes = [1608, 1608, 2048, 700, 1608, 0, 1]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    P = synth(rng, int(offs[-1]), 4, 4, np.float32)
+    P[offs[0]:offs[1]] = 0.25                                  # all equal
+    P[offs[1]:offs[2]] = np.where(rng.random((1608, 1, 1)) < 0.5, 0.25, [0.7, 0.1, 0.1, 0.1])
+    P[offs[4] + rng.integers(0, 1608, 40)] = np.nan            # NaN rows rank first
+    ent_o = O.oracle_committee_entropy(P, "NMC")
+    Pm = dev(np.ascontiguousarray(np.transpose(P, (1, 0, 2))))
+    for q in (10, 64):
+        _, idx = ce.ops.select_batched(Pm, dev(offs), q, "MNC")
+        idx = idx.cpu().numpy()
+        for u in range(len(sizes)):
+            io = O.oracle_topq(ent_o[offs[u]:offs[u + 1]], q)[1]
+            assert np.array_equal(idx[u][idx[u] >= 0], io), (q, u)
+
+
 @pytest.mark.parametrize("nl,q", [(1, 10), (3, 1), (64, 10), (1024, 10), (1024, 64), (5000, 17)])
 def test_merge_lists_vs_oracle(ce, nl, q):
     """Stage-2 merge (register lists, 16 waves) over many best-first lists,

@@ -51,6 +51,8 @@ def test_new_entry_points_validate_without_gpu():
     # member inference: too many features / classes, inconsistent K
     rc = lib.ce_gnb_predict_proba(p, 10, 513, 513, p, p, p, 4, p, 4, None)
     assert rc == _lib.CE_EINVAL
+    for D in range(1, 8):  # fewer than 8 features: numpy's sequential sum, not the 8-lane plan
+        assert lib.ce_gnb_predict_proba(p, 10, D, D, p, p, p, 4, p, 4, None) == _lib.CE_EUNSUPPORTED
     rc = lib.ce_sgd_predict_proba(p, 10, 260, 260, p, p, 3, 4, p, 4, None)
     assert rc == _lib.CE_EINVAL
     assert lib.ce_mark_selected(None, 10, p, 1, 0, None) == _lib.CE_EINVAL
@@ -66,3 +68,17 @@ def test_python_guards_without_gpu():
         ops.gnb_predict_proba(torch.zeros((4, 4), dtype=torch.float64), np.zeros((2, 4)), np.ones((2, 4)), [0.5, 0.5])
     with pytest.raises(ValueError, match="HIP device"):
         ops.merge_cands(torch.zeros((10, 2), dtype=torch.int64), 10)
+
+
+def test_select_queries_guards_without_gpu():
+    from ce_amd import select_queries
+    from ce_amd.select import ConsensusEntropySelector
+
+    with pytest.raises(ValueError, match="CE_MAX_Q"):
+        select_queries("mc", 2049, committee=[np.zeros((3, 4))])
+    with pytest.raises(ValueError, match="mode"):
+        ConsensusEntropySelector(10, "qbc")
+    sel = ConsensusEntropySelector(10, "mc")
+    for empty in (None, [], np.zeros((0, 5, 4))):
+        with pytest.raises(ValueError, match="pred_prob"):
+            sel.select(pred_prob=empty)

@@ -48,10 +48,10 @@ def transform(marg, G):
         for v in row[1:]:
             mx = v if v > mx else mx
         e = [O.libm_expf(np.float32(v - mx)) for v in row]
-        ws = np.float32(0)
+        ws = 0.0  # xgboost common::Softmax: `double wsum`, Python float = IEEE double
         for v in e:
-            ws = np.float32(ws + v)
-        out[r] = [np.float32(v / ws) for v in e]
+            ws += float(v)
+        out[r] = [np.float32(v / np.float32(ws)) for v in e]
     return out
 
 
@@ -122,10 +122,32 @@ def test_restated_expf_matches_libm():
     assert np.array_equal(O.oracle_expf(hard).view(np.uint32), np.array([O.libm_expf(v) for v in hard]).view(np.uint32))
 
 
+def test_softmax_accumulator_discriminates():
+    """xgboost's common::Softmax sums the float32 exps in a DOUBLE and divides by
+    its float32 cast; a float32 running sum rounds differently on some rows, so
+    the walk above (double) and the oracle/device (double) are checked against
+    a choice that matters."""
+    rng = np.random.default_rng(3)
+    differ = 0
+    for row in rng.normal(0, 3, (4000, 4)).astype(np.float32):
+        mx = max(row)
+        e = [O.libm_expf(np.float32(v - mx)) for v in row]
+        wf = np.float32(0)
+        for v in e:
+            wf = np.float32(wf + v)
+        wd = np.float32(sum(float(v) for v in e))
+        differ += wf != wd
+    assert differ > 0
+
+
 def test_model_errors():
     model = synthetic_model(n_rounds=2, num_class=4, max_depth=3, num_feature=8, seed=0)
     bad = json.loads(json.dumps(model))
     bad["learner"]["objective"]["name"] = "reg:squarederror"
+    with pytest.raises(ValueError, match="objective"):
+        XgbForest.from_json(bad)
+    bad = json.loads(json.dumps(model))
+    bad["learner"]["objective"]["name"] = "multi:softmax"  # predict_proba would be [1 - label, label]
     with pytest.raises(ValueError, match="objective"):
         XgbForest.from_json(bad)
     bad = json.loads(json.dumps(model))

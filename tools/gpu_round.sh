@@ -49,6 +49,15 @@ profile)
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/write_$LAYOUT" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --layout "$LAYOUT" > "$OUT/prof_write_$LAYOUT.log" 2>&1
   step $? "write $LAYOUT"
   ;;
+benchprof)  # rocprofv3 kernel trace of EXACTLY the driver's bench command (its JSON line on stdout)
+  cd /tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof/bench_exact" -o run --output-format csv -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_exact.json" 2> "$OUT/bench_exact.err"
+  step $? "trace bench exact"
+  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/fetch_NMC" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_fetch_NMC.log" 2>&1
+  step $? "fetch NMC"
+  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/write_NMC" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_write_NMC.log" 2>&1
+  step $? "write NMC"
+  ;;
 configs)  # kernel-trace stats of every secondary config + FETCH/WRITE passes of the wide one
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof/configs" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" > "$OUT/prof_configs.log" 2>&1
@@ -65,6 +74,6 @@ xgb)  # kernel-trace stats + FETCH_SIZE pass of the XGB member (bench_configs --
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/fetch_xgb" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" --only 7 > "$OUT/prof_fetch_xgb.log" 2>&1
   step $? "fetch xgb"
   ;;
-*) echo "PHASE must be check, ab, profile, configs or xgb" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs or xgb" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
