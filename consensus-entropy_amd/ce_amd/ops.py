@@ -366,6 +366,61 @@ def merge_cands(cands, q):
     return ov, oi
 
 
+class MCChunkJob:
+    """amg_test.py:441-445 over a pool larger than HBM (BASELINE configs[4]),
+    streamed as consecutive chunks: ``add(P_chunk)`` scores one resident chunk
+    (pool positions continue from the previous chunk) and folds its top-q into
+    a running list of q candidate records on the device; ``result()`` is the
+    selection over everything added -- identical to select_mc on the whole
+    pool, ties included (q <= 64)."""
+
+    def __init__(self, q, layout="NMC", device=None):
+        self.q = _check_q(q)
+        if self.q > _lib.CE_CAND_MAX_Q:
+            raise ValueError(f"chunked selection needs q <= {_lib.CE_CAND_MAX_Q}")
+        self.layout = layout
+        self.device = torch.device(device) if device is not None else None
+        self.running = None
+        self.n_items = 0
+        self._fresh = True
+
+    def add(self, P, base_idx=None):
+        """Score chunk P (layout as constructed); its items are pool positions
+        base_idx .. base_idx + N - 1 (default: right after the previous chunk)."""
+        N, M, C, sN, sM, sC, dt = committee_view(P, self.layout)
+        if self.running is None:
+            self.running = torch.empty((self.q, 2), dtype=torch.int64, device=P.device)
+        base = self.n_items if base_idx is None else int(base_idx)
+        lib = _lib.load()
+        ws = WORKSPACE.get(P.device, lib.ce_select_mc_chunk_workspace_bytes(N, self.q))
+        first = 1 if self._fresh else 0
+        call("ce_select_mc_chunk", _p(P), dt, N, M, C, sN, sM, sC, self.q, base, _p(self.running), first, _p(ws),
+             ws.numel(), _stream(P.device))
+        self._fresh = False
+        self.n_items = max(self.n_items, base + N)
+        return self
+
+    def result(self):
+        """(vals [q], idx [q]) best-first over every chunk added (idx -1 padding)."""
+        if self.running is None:
+            raise ValueError("no chunk added")
+        return merge_cands(self.running, self.q)
+
+
+def select_mc_chunks(chunks, q, layout="NMC"):
+    """Convenience over MCChunkJob: ``chunks`` yields consecutive device tensors
+    (or (tensor, base_idx) pairs) of one pool."""
+    job = None
+    for ch in chunks:
+        P, base = ch if isinstance(ch, tuple) else (ch, None)
+        if job is None:
+            job = MCChunkJob(q, layout, P.device)
+        job.add(P, base)
+    if job is None:
+        raise ValueError("no chunks")
+    return job.result()
+
+
 def select_mix(P, hc, q, layout="MNC"):
     """Fused amg_test.py:473-480: top-q over the row stack [mc (N); hc (N_h)]."""
     N, M, C, sN, sM, sC, dt = committee_view(P, layout)

@@ -1612,6 +1612,48 @@ extern "C" int ce_merge_cands(const ce_cand* c, int32_t nlists, int32_t q, doubl
     return check_launch("ce_merge_cands");
 }
 
+// ---- chunked pools (larger than HBM) ----------------------------------------
+__global__ void k_cand_empty(Cand* __restrict__ c, int q) {
+    for (int r = threadIdx.x; r < q; r += blockDim.x) c[r] = Cand{0ull, -1};
+}
+
+extern "C" size_t ce_select_mc_chunk_workspace_bytes(int64_t N, int32_t q) {
+    return lists_bytes((int64_t)pool_blocks(N) + 1, q < 1 ? 1 : q);
+}
+
+// Stage 1 on the chunk (its G block lists), then ONE merge of those G lists
+// plus the running list (copied to list slot G of the workspace) back into
+// `running`: the running list always holds the top-q of every chunk so far
+// (the top-q of a union is within the union of the parts' top-qs).
+extern "C" int ce_select_mc_chunk(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                                  int64_t sM, int64_t sC, int32_t q, int64_t base_idx, ce_cand* running,
+                                  int32_t first, void* ws, size_t ws_bytes, ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "chunked selection needs q <= %d (got %d)", kStreamMaxQ, q);
+    if (!running || (uintptr_t)running % 16) return fail(CE_EINVAL, "running list must be 16-byte aligned device memory");
+    if (N < 0 || base_idx < 0) return fail(CE_EINVAL, "bad chunk N=%lld base_idx=%lld", (long long)N, (long long)base_idx);
+    hipStream_t st = (hipStream_t)stream;
+    Cand* run = reinterpret_cast<Cand*>(running);
+    if (N == 0) {
+        if (first) hipLaunchKernelGGL(k_cand_empty, dim3(1), dim3(64), 0, st, run, q);
+        return check_launch("ce_select_mc_chunk");
+    }
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes((int64_t)G + 1, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    WsLists w = carve(ws, (int64_t)G + 1, q);
+    if (!first && hipMemcpyAsync(w.c + (int64_t)G * q, run, (size_t)q * sizeof(Cand), hipMemcpyDeviceToDevice, st) !=
+                      hipSuccess)
+        return fail(CE_ELAUNCH, "running-list copy failed");
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int Gs = 0;
+    bool fin = false;
+    rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &Gs, &fin, st);
+    if (rc) return rc;
+    launch_finish(ListSrc<false>{w.c, nullptr, nullptr}, 1, G + (first ? 0 : 1), q, nullptr, nullptr, st, run);
+    return check_launch("ce_select_mc_chunk");
+}
+
 // ---- fused mix ---------------------------------------------------------------
 extern "C" size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t q) {
     return lists_bytes((int64_t)pool_blocks(N) + pool_blocks(N_h), q < 1 ? 1 : q);

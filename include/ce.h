@@ -222,6 +222,22 @@ int ce_merge_cands(const ce_cand *c, int32_t nlists, int32_t q, double *val_out,
                    ce_stream_t stream);
 
 /*
+ * Chunked mc selection for a pool larger than HBM (BASELINE configs[4]: 50M
+ * items x 32 members x 1000 classes bf16 = 3.2 TB) -- amg_test.py:441-445 over
+ * a pool that arrives in chunks.  Each call scores one resident chunk (pool
+ * items base_idx .. base_idx + N - 1, positions reported as pool positions)
+ * and merges its top-q with the caller's running list `running` (q ce_cand
+ * records, best first, 16-byte aligned device memory) in place; first != 0
+ * starts a job (running's content is ignored and overwritten).  After the
+ * last chunk ce_merge_cands(running, 1, q, ...) returns the selection -- the
+ * same as ce_select_mc over the whole pool, ties included.  q <= 64.
+ */
+size_t ce_select_mc_chunk_workspace_bytes(int64_t N, int32_t q);
+int ce_select_mc_chunk(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                       int64_t sM, int64_t sC, int32_t q, int64_t base_idx, ce_cand *running,
+                       int32_t first, void *ws, size_t ws_bytes, ce_stream_t stream);
+
+/*
  * Device-resident multi-epoch selection (amg_test.py:396-397
  * epochs, :455/:484 hc-pool shrink, :521-531 X_train shrink): instead of
  * rebuilding the pool every epoch, the caller keeps the full pool on the device

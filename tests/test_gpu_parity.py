@@ -738,3 +738,38 @@ def test_gnb_widest_shape(ce):
     X = theta[rng.integers(0, C, 3000)] + rng.normal(0, 1, (3000, D)) * np.sqrt(var[0])
     got = ce.ops.gnb_predict_proba(dev(X), theta, var, prior).cpu().numpy()
     np.testing.assert_allclose(got, ref_gnb_predict_proba(X, theta, var, prior), rtol=1e-10, atol=1e-300)
+
+
+@pytest.mark.parametrize("C,dt,N,chunk", [(4, "f32", 300_000, 50_000), (1000, "bf16", 6_000, 1_000),
+                                          (4, "f64", 70_001, 9_999)])
+def test_chunked_pool_vs_oracle(ce, C, dt, N, chunk):
+    """ce_select_mc_chunk (pools larger than HBM, BASELINE configs[4]): >= 6
+    chunks scored one at a time into a running top-q equal the oracle's
+    selection over the whole pool.  Exact ties straddle every chunk boundary
+    (the same rows repeated on both sides, the later copy must lose) and the
+    pool is quantised so ties cross the q-th place."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(C + N)
+    M = 32 if C == 1000 else 16
+    P = synth(rng, N, M, C, np.float32, quant=None if C == 1000 else 16)
+    for b in range(chunk, N, chunk):  # identical maximal-entropy rows on both sides of each boundary
+        P[b - 2:b + 2] = 1.0 / C
+    if dt == "bf16":
+        host = _bf16_bits(P)
+        Pd = dev(host.view(np.int16)).view(torch.bfloat16)
+    else:
+        host = P.astype(np.float64) if dt == "f64" else P
+        Pd = dev(host)
+    ent_o = O.oracle_committee_entropy(host, "NMC")
+    for q in (10, 64):
+        _, idx_o = O.oracle_topq(ent_o, q)
+        job = ce.ops.MCChunkJob(q, "NMC")
+        for lo in range(0, N, chunk):
+            job.add(Pd[lo:lo + chunk])
+        _, idx = job.result()
+        assert np.array_equal(idx_np(idx), idx_o), q
+    # chunks handed in out of order with explicit positions: same answer
+    chunks = [(Pd[lo:lo + chunk], lo) for lo in range(0, N, chunk)][::-1]
+    _, idx = ce.ops.select_mc_chunks(chunks, 10, "NMC")
+    assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
