@@ -136,7 +136,8 @@ def cpu_baseline_multicore(n_items, M, C, q, seed=1987, procs=None):
 
     from oracle.ce_oracle import ref_mc_shard_time
 
-    procs = procs or max(1, min(16, os.cpu_count() or 1))
+    share = host_cpu_share()
+    procs = procs or share["usable"]
     n = max(1, n_items // 4)
     env_old = os.environ.get("OMP_NUM_THREADS")
     os.environ["OMP_NUM_THREADS"] = "1"  # inherited by the spawned workers
@@ -149,8 +150,48 @@ def cpu_baseline_multicore(n_items, M, C, q, seed=1987, procs=None):
         else:
             os.environ["OMP_NUM_THREADS"] = env_old
     t = max(r[0] for r in res)
-    return {"value": sum(r[1] for r in res) / t, "unit": "items/s", "cores": procs,
-            "sample": f"{procs} spawned single-threaded workers x {n} items each, median of 3 per worker"}
+    rate = sum(r[1] for r in res) / t
+    out = {"value": rate, "unit": "items/s", "cores": procs,
+           "sample": f"{procs} spawned single-threaded workers x {n} items each, median of 3 per worker",
+           "host": share}
+    if share["physical_cores"]:
+        # the job's CPU share is `usable` cores; the whole machine's physical cores, at
+        # the measured per-core rate (numpy here is per-core compute-bound), would give:
+        out["extrapolated_all_physical_cores"] = {"value": rate / procs * share["physical_cores"],
+                                                  "cores": share["physical_cores"], "kind": "linear extrapolation"}
+    return out
+
+
+def host_cpu_share():
+    """CPUs this job may use: the affinity mask, the cgroup CPU quota, and the
+    GPU pool's rule of 16 host CPUs per GPU; plus the machine's physical cores
+    (sockets x cores per socket from /proc/cpuinfo) for the record."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    phys = set()
+    try:
+        pid = core = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+                phys.add((pid, core))
+    except OSError:
+        pass
+    usable = min(x for x in (affinity, quota or affinity, 16) if x)
+    return {"usable": usable, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "logical_cpus": os.cpu_count(), "physical_cores": len(phys) or None,
+            "rule": "GPU pool: 16 host CPUs per GPU job"}
 
 
 def main():

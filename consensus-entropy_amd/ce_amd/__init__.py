@@ -12,11 +12,11 @@ from .select import (MODES, ConsensusEntropySelector, committee_from_frames, sel
 from .session import SelectionSession  # noqa: F401,E402
 
 __all__ = ["SelectionSession", "select_queries", "ConsensusEntropySelector", "stack_committee", "committee_from_frames", "song_groups",
-           "MODES", "CE_MAX_Q", "CEError", "load", "ops", "dist"]
+           "MODES", "CE_MAX_Q", "CEError", "load", "ops", "dist", "torch_ops"]
 
 
 def __getattr__(name):  # lazy submodules (ops/dist need torch)
-    if name in ("ops", "dist"):
+    if name in ("ops", "dist", "torch_ops"):
         import importlib
 
         return importlib.import_module(f".{name}", __name__)

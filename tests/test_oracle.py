@@ -15,6 +15,8 @@ import pytest
 from conftest import GOLDEN, golden
 from oracle import ce_oracle as O
 
+ORACLE_DIR = os.path.dirname(os.path.abspath(O.__file__))
+
 MC_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "mc_*.npz")))
 
 
@@ -181,3 +183,17 @@ def test_member_restatements_vs_sklearn():
     np.testing.assert_allclose(p, gnb.predict_proba(Xt), rtol=1e-9, atol=1e-300)
     p = ref_sgd_predict_proba(Xt, sgd.coef_, sgd.intercept_)
     np.testing.assert_allclose(p, sgd.predict_proba(Xt), rtol=1e-9, atol=1e-300)
+
+
+def test_oracle_under_sanitizers():
+    """the C restatement under host ASan + UBSan (oracle/Makefile
+    `sanitize`: every ce_ref_* entry point on edge-case inputs; any finding
+    aborts)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("gcc") is None and shutil.which("cc") is None:
+        pytest.skip("no C compiler")
+    r = subprocess.run(["make", "-s", "-C", ORACLE_DIR, "sanitize"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "sanitized oracle run: ok" in r.stdout
