@@ -1102,8 +1102,17 @@ template <class Src, int BS>
 static void launch_small(const Src& src, int grid, const int64_t* offsets, int64_t n, int64_t base_idx, int q,
                          double* oval, int64_t* oidx, const uint32_t* excl, hipStream_t st) {
     constexpr int UNR = (Src::kDT == kF64 || Src::kC > 4 || BS > kSmallBS) ? 2 : 4;
-    hipLaunchKernelGGL((k_select_small<Src, small_ipt<Src>(), UNR, BS>), dim3((unsigned)grid), dim3(BS), 0, st, src,
-                       offsets, n, base_idx, q, oval, oidx, excl);
+    hipLaunchKernelGGL((k_select_small<Src, Src, small_ipt<Src>(), 0, UNR, 1, BS>), dim3((unsigned)grid), dim3(BS), 0,
+                       st, src, src, offsets, n, (int64_t)0, base_idx, q, oval, oidx, excl);
+}
+// mix in one block: committee items (A) then the hc table rows (B, a 1-member
+// f64 committee); IPT 2 per segment at 1024 threads: up to 2048 + 2048 rows
+template <class SrcA, class SrcB>
+static void launch_small_mix(const SrcA& a, const SrcB& b, int64_t n, int64_t nB, int q, double* oval,
+                             int64_t* oidx, hipStream_t st) {
+    constexpr int UNRA = (SrcA::kDT == kF64 || SrcA::kC > 4) ? 2 : 4;
+    hipLaunchKernelGGL((k_select_small<SrcA, SrcB, 2, 2, UNRA, 1, kSmallBSWide>), dim3(1), dim3(kSmallBSWide), 0, st, a,
+                       b, (const int64_t*)nullptr, n, nB, (int64_t)0, q, oval, oidx, (const uint32_t*)nullptr);
 }
 static bool small_enabled() {
     static int v = -1;
@@ -1673,6 +1682,24 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     if (!ws || ws_bytes < lists_bytes((int64_t)G1 + G2, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, (int64_t)G1 + G2, q);
+    if (small_enabled() && q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= 2 * kSmallBSWide &&
+        N_h <= 2 * kSmallBSWide && (C == 4 || C == 8)) {
+        // both segments in ONE block (k_select_small, two segments)
+        const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
+        bool launched = false;
+        rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            if constexpr (S::kC == 4 || S::kC == 8) {
+                constexpr int CC = S::kC;
+                if (vec_ok(t, CC))
+                    launch_small_mix(src, make_src<kF64, CC, true>(t), N, N_h, q, val_out, idx_out, st);
+                else
+                    launch_small_mix(src, make_src<kF64, CC, false>(t), N, N_h, q, val_out, idx_out, st);
+                launched = true;
+            }
+        });
+        if (rc == CE_OK && launched) return check_launch("ce_select_mix");
+    }
     // both segments on the streaming engine when it applies (q <= 64): the hc
     // table is a committee of M = 1 member ([N_h, 1, C] f64, row stride ld_hc)
     if (!launch_stream(a, G1, q, 0, w, st)) {

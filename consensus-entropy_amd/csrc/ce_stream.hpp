@@ -623,11 +623,15 @@ struct SmallSmem {
     WaveListsT<WAVES> lists;                // fallback tree merge
 };
 
-template <class Src, int IPT, int UNR, int BS>
+// Two segments in one block (SrcB, IPTB > 0: the mix of amg_test.py:473-480,
+// committee items then hc rows): segment A's items keep positions item + rel,
+// segment B's rows [0, nB) follow at n + base_idx + j; one selection over both.
+template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_select_small(
-    Src src, const int64_t* __restrict__ offsets, int64_t n, int64_t base_idx, int q, double* __restrict__ oval,
-    int64_t* __restrict__ oidx, const uint32_t* __restrict__ excl) {
+    SrcA srcA, SrcB srcB, const int64_t* __restrict__ offsets, int64_t n, int64_t nB, int64_t base_idx, int q,
+    double* __restrict__ oval, int64_t* __restrict__ oidx, const uint32_t* __restrict__ excl) {
     constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
+    constexpr int K = IPTA + IPTB, IB = IPTB > 0 ? IPTB : 1;
     static_assert(BS % 64 == 0 && BS >= 128 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
     using SM = SmallSmem<W>;
     __shared__ SM sm;
@@ -639,51 +643,88 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int64_t s0 = offsets ? offsets[u] : 0, s1 = offsets ? offsets[u + 1] : n;
     const int64_t len = s1 > s0 ? s1 - s0 : 0;
     const int64_t rel = (offsets ? 0 : base_idx) - s0;  // position = item + rel
+    const int64_t relB = n + base_idx;                  // segment B: position = row + relB
+    if constexpr (IPTB == 0) nB = 0;
     double* ov = oval + (int64_t)u * q;
     int64_t* oi = oidx + (int64_t)u * q;
-    if (len > (int64_t)BS * IPT) {  // long pool: per-wave streams + tree merge (block-uniform)
+    if (len > (int64_t)BS * IPTA || nB > (int64_t)BS * IPTB) {  // long pools: per-wave streams + tree merge
         tab.commit();
         constexpr int64_t kIt = 64 * 2;
-        const int64_t its = (len + kIt - 1) / kIt, its_w = (its + W - 1) / W;
-        int64_t lo = s0 + (int64_t)w * its_w * kIt;
-        int64_t hi = lo + its_w * kIt < s1 ? lo + its_w * kIt : s1;
-        if (lo > hi) lo = hi;
         RegTopQ tq;
         tq.init(q);
-        stream_direct_range<Src, 2, UNR>(src, lo, hi, rel, q, tq, excl);
+        {
+            const int64_t its = (len + kIt - 1) / kIt, its_w = (its + W - 1) / W;
+            int64_t lo = s0 + (int64_t)w * its_w * kIt;
+            int64_t hi = lo + its_w * kIt < s1 ? lo + its_w * kIt : s1;
+            if (lo > hi) lo = hi;
+            stream_direct_range<SrcA, 2, UNRA>(srcA, lo, hi, rel, q, tq, excl);
+        }
+        if constexpr (IPTB > 0) {
+            const int64_t its = (nB + kIt - 1) / kIt, its_w = (its + W - 1) / W;
+            int64_t lo = (int64_t)w * its_w * kIt;
+            int64_t hi = lo + its_w * kIt < nB ? lo + its_w * kIt : nB;
+            if (lo > hi) lo = hi;
+            stream_direct_range<SrcB, 2, UNRB>(srcB, lo, hi, relB, q, tq, nullptr);
+        }
         block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
         return;
     }
-    // 1. keys of this thread's IPT items, every load in flight before any math
-    int64_t items[IPT];
-    uint64_t k[IPT];
-    bool ok[IPT];
+    // 1. keys of this thread's items, every load of a segment in flight before its math
+    uint64_t k[K];
+    int64_t pos[K];
+    bool ok[K];
+    {
+        int64_t items[IPTA];
+        uint64_t ka[IPTA];
+        int nlive = 0;  // this wave's item slots holding at least one real item (a prefix)
 #pragma unroll
-    for (int v = 0; v < IPT; ++v) {
-        const int64_t j = tid + (int64_t)BS * v;
-        items[v] = s0 + (j < len ? j : (len > 0 ? len - 1 : 0));
-        k[v] = 0;
+        for (int v = 0; v < IPTA; ++v) {
+            const int64_t j = tid + (int64_t)BS * v;
+            items[v] = s0 + (j < len ? j : (len > 0 ? len - 1 : 0));
+            ka[v] = 0;
+            nlive += (int64_t)BS * v + 64 * w < len;
+        }
+        if (len > 0) {  // block-uniform
+            srcA.template keys_small<UNRA, IPTA>(items, ka, nlive, [&]() { tab.commit(); });
+        } else {
+            tab.commit();
+        }
+#pragma unroll
+        for (int v = 0; v < IPTA; ++v) {
+            k[v] = ka[v];
+            pos[v] = items[v] + rel;
+            ok[v] = tid + (int64_t)BS * v < len;
+            if (excl) ok[v] = ok[v] && !excluded(excl, items[v]);
+        }
     }
-    int nlive = 0;  // this wave's item slots holding at least one real item (a prefix)
+    if constexpr (IPTB > 0) {
+        int64_t rows[IB];
+        uint64_t kb[IB];
+        int nlive = 0;
 #pragma unroll
-    for (int v = 0; v < IPT; ++v) nlive += (int64_t)BS * v + 64 * w < len;
-    if (len > 0) {  // block-uniform
-        src.template keys_small<UNR, IPT>(items, k, nlive, [&]() { tab.commit(); });
-    } else {
-        tab.commit();
+        for (int v = 0; v < IPTB; ++v) {
+            const int64_t j = tid + (int64_t)BS * v;
+            rows[v] = j < nB ? j : (nB > 0 ? nB - 1 : 0);
+            kb[v] = 0;
+            nlive += (int64_t)BS * v + 64 * w < nB;
+        }
+        if (nB > 0) srcB.template keys_small<UNRB, IPTB>(rows, kb, nlive);
+#pragma unroll
+        for (int v = 0; v < IPTB; ++v) {
+            k[IPTA + v] = kb[v];
+            pos[IPTA + v] = rows[v] + relB;
+            ok[IPTA + v] = tid + (int64_t)BS * v < nB;
+        }
     }
     CE_STAMP(u, 1)
     uint64_t bk = 0;
     int64_t bi = INT64_MAX;
 #pragma unroll
-    for (int v = 0; v < IPT; ++v) {
-        ok[v] = tid + (int64_t)BS * v < len;
-        if (excl) ok[v] = ok[v] && !excluded(excl, items[v]);
-        if (ok[v] && better(k[v], items[v] + rel, bk, bi)) {
+    for (int v = 0; v < K; ++v)
+        if (ok[v] && better(k[v], pos[v], bk, bi)) {
             bk = k[v];
-            bi = items[v] + rel;
+            bi = pos[v];
         }
-    }
     // 2. floor = the group best of rank q-1 (ranks split over the waves)
     group_best<GS>(bk, bi);
     if ((tid & (GS - 1)) == 0) {
@@ -720,9 +761,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     CE_STAMP(u, 2)
     // 3. survivors (not worse than the floor) -> LDS list
 #pragma unroll
-    for (int v = 0; v < IPT; ++v) {
-        const int64_t pos = items[v] + rel;
-        const bool pass = ok[v] && !better(fk, fi, k[v], pos);
+    for (int v = 0; v < K; ++v) {
+        const bool pass = ok[v] && !better(fk, fi, k[v], pos[v]);
         const uint64_t m = __ballot(pass);
         if (m) {  // wave-uniform
             int base = 0;
@@ -732,7 +772,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
             if (pass && slot < SM::CAP) {
                 sm.ck[slot] = k[v];
-                sm.ci[slot] = pos;
+                sm.ci[slot] = pos[v];
             }
         }
     }
@@ -760,7 +800,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     RegTopQ tq;
     tq.init(q, fk, fi == INT64_MAX ? fi : fi + 1);  // admit candidates >= the floor
 #pragma unroll
-    for (int v = 0; v < IPT; ++v) tq.offer(k[v], items[v] + rel, ok[v]);
+    for (int v = 0; v < K; ++v) tq.offer(k[v], pos[v], ok[v]);
     block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
 }
 

@@ -22,6 +22,42 @@ import ce_amd.ops as ops  # noqa: E402
 PEAK = 8000.0
 
 
+def run(items=50_000_000, chunk=250_000, members=32, classes=1000, q=10, log=True):
+    M, C, Nc = members, classes, chunk
+    bufs = [torch.empty((min(Nc, items), M, C), dtype=torch.bfloat16, device="cuda") for _ in range(2)]
+    job = ops.MCChunkJob(q, "NMC")
+    evs = []
+    nch = (items + Nc - 1) // Nc
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for c in range(nch):
+        lo = c * Nc
+        n = min(Nc, items - lo)
+        buf = bufs[c & 1][:n]
+        buf.uniform_(0.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1987 * 100_003 + c))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        job.add(buf)
+        e1.record()
+        evs.append((e0, e1))
+        if log and c % 20 == 0:
+            print(f"chunk {c}/{nch}", file=sys.stderr, flush=True)
+    vals, idx = job.result()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    score_s = sum(e0.elapsed_time(e1) for e0, e1 in evs) * 1e-3
+    nbytes = items * M * C * 2
+    del bufs
+    torch.cuda.empty_cache()
+    return {
+        "config": f"configs[4] wide-class job: {items} items x {M} x {C} bf16 ({nbytes / 1e12:.2f} TB), "
+                  f"{nch} device-generated chunks of {Nc}, running top-{q}",
+        "items": items, "chunks": nch, "score_s": score_s, "items_per_s": items / score_s,
+        "GB_per_s": nbytes / score_s / 1e9, "frac_hbm": nbytes / score_s / 1e9 / PEAK,
+        "wall_s_incl_generation": wall,
+        "selected": idx.cpu().tolist(), "entropies": vals.cpu().tolist()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--items", type=int, default=50_000_000)
@@ -30,37 +66,7 @@ def main():
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--q", type=int, default=10)
     a = ap.parse_args()
-    M, C, Nc = a.members, a.classes, a.chunk
-    bufs = [torch.empty((Nc, M, C), dtype=torch.bfloat16, device="cuda") for _ in range(2)]
-    job = ops.MCChunkJob(a.q, "NMC")
-    evs = []
-    nch = (a.items + Nc - 1) // Nc
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for c in range(nch):
-        lo = c * Nc
-        n = min(Nc, a.items - lo)
-        buf = bufs[c & 1][:n]
-        buf.uniform_(0.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1987 * 100_003 + c))
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        job.add(buf)
-        e1.record()
-        evs.append((e0, e1))
-        if c % 20 == 0:
-            print(f"chunk {c}/{nch}", file=sys.stderr, flush=True)
-    vals, idx = job.result()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    score_s = sum(e0.elapsed_time(e1) for e0, e1 in evs) * 1e-3
-    nbytes = a.items * M * C * 2
-    print(json.dumps({
-        "config": f"configs[4] wide-class job: {a.items} items x {M} x {C} bf16 ({nbytes / 1e12:.2f} TB), "
-                  f"{nch} device-generated chunks of {Nc}, running top-{a.q}",
-        "items": a.items, "chunks": nch, "score_s": score_s, "items_per_s": a.items / score_s,
-        "GB_per_s": nbytes / score_s / 1e9, "frac_hbm": nbytes / score_s / 1e9 / PEAK,
-        "wall_s_incl_generation": wall,
-        "selected": idx.cpu().tolist(), "entropies": vals.cpu().tolist()}), flush=True)
+    print(json.dumps(run(a.items, a.chunk, a.members, a.classes, a.q)), flush=True)
 
 
 if __name__ == "__main__":

@@ -204,20 +204,10 @@ def main():
         Pr = P[:, :n].contiguous()
         t = timed(lambda: ops.select_batched(Pr, offs_r, q, "MNC"), 50)
         report("configs[2] batched ragged 500 users (N_u in [128,1608])", n, Pr.numel() * 4, t)
-    if 4 in only:  # configs[4]: 50M x 32 x 1000 bf16 (3.2 TB): one resident chunk, re-scored per chunk
-        Nc, M, C = 200_000, 32, 1000
-        chunk = torch.empty((Nc, M, C), dtype=torch.bfloat16, device="cuda")
-        for s in range(0, Nc, 20_000):
-            chunk[s:s + 20_000] = dirichlet((20_000, M, C), torch.bfloat16, g)
-        torch.cuda.synchronize()
-        total = 50_000_000
-        nchunks = 5
-        t0 = time.time()
-        t = timed(lambda: ops.select_mc(chunk, q, "NMC"), nchunks)
-        report("configs[4] wide 32x1000 bf16, per 200K-item chunk", Nc, chunk.numel() * 2, t,
-               {"est_full_50M_s": t * total / Nc, "wall": time.time() - t0})
-        del chunk
-        torch.cuda.empty_cache()
+    if 4 in only:  # configs[4]: 50M x 32 x 1000 bf16 (3.2 TB) streamed in chunks; here the first 5M items
+        from tools.bench_c5 import run as c5_run
+
+        print(json.dumps(c5_run(items=5_000_000, log=False)), flush=True)  # full job: tools/bench_c5.py
     if 5 in only:
         segment_mean_configs(g, report)
     if 6 in only:  # §8(f)4: member inference over 260-feature frames (GNB, SGD log), C = 4
