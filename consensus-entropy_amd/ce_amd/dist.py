@@ -106,3 +106,22 @@ def sharded_select_mc(P_local, q, *, global_offset, layout="NMC", group=None, lo
         return vals, idx
     all_vals, all_idx = allgather_topq(vals, idx, q, group)
     return merge(all_vals, all_idx, q)
+
+
+def sharded_select_mc_chunks(chunks, q, *, layout="NMC", group=None, job=None, merge_records=None):
+    """A pool larger than HBM (BASELINE configs[4]) over several GPUs: this
+    rank streams ITS chunks -- ``chunks`` yields (device tensor, global
+    base_idx) pairs, e.g. chunk c on rank c % world -- into a running top-q
+    (ops.MCChunkJob, q <= 64), then ONE all-gather of every rank's q running
+    records and the same merge on every rank.  A rank with no chunk contributes
+    an empty list.  ``job``/``merge_records`` are injectable for CPU tests."""
+    if job is None:
+        job = ops.MCChunkJob(q, layout)
+    if merge_records is None:
+        merge_records = ops.merge_cands
+    for P, base in chunks:
+        job.add(P, base)
+    rec = job.running_records()
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        rec = allgather_cands(rec, group)
+    return merge_records(rec, q)

@@ -400,6 +400,17 @@ class MCChunkJob:
         self.n_items = max(self.n_items, base + N)
         return self
 
+    def running_records(self, device=None):
+        """The running list: q candidate records (int64 [q, 2], best first; an
+        empty list -- key 0, idx -1 -- when no chunk was added), e.g. the send
+        buffer of the multi-GPU all-gather."""
+        if self.running is None:
+            dev = device if device is not None else (self.device or torch.device("cuda", torch.cuda.current_device()))
+            empty = torch.zeros((self.q, 2), dtype=torch.int64, device=dev)
+            empty[:, 1] = -1
+            return empty
+        return self.running
+
     def result(self):
         """(vals [q], idx [q]) best-first over every chunk added (idx -1 padding)."""
         if self.running is None:

@@ -174,3 +174,58 @@ def test_pack_roundtrip():
     vv, ii = unpack(buf, 4, 2)
     assert torch.equal(ii, torch.cat([i, i + 100]))
     assert torch.allclose(vv, torch.cat([v, v * 2]), equal_nan=True)
+
+
+class _OracleChunkJob:
+    """MCChunkJob's contract restated with the oracle: a running list of q
+    records folded with each chunk's top-q (the CPU stand-in for the HIP job)."""
+
+    def __init__(self, q):
+        self.q = q
+        self.rec = None
+
+    def add(self, P, base):
+        r = _oracle_local_records(P, self.q, base)
+        if self.rec is not None:
+            v, i = _oracle_merge_records(torch.cat([self.rec, r]), self.q)
+            r = torch.from_numpy(np.stack([np.where(i.numpy() >= 0, _order_key(v.numpy()), 0).view(np.int64)
+                                           if len(i) else np.zeros(0, np.int64), i.numpy()], 1))
+            pad = self.q - r.shape[0]
+            if pad:
+                r = torch.cat([r, torch.tensor([[0, -1]] * pad, dtype=torch.int64)])
+        self.rec = r
+
+    def running_records(self):
+        if self.rec is None:
+            return torch.tensor([[0, -1]] * self.q, dtype=torch.int64)
+        return self.rec
+
+
+def _worker_chunks(rank, world, port, N, chunk, q, seed, out):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "consensus-entropy_amd"))
+    from ce_amd import dist as cdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P = _pool(N, seed)
+    mine = [(torch.from_numpy(P[lo:lo + chunk]), lo) for c, lo in enumerate(range(0, N, chunk)) if c % world == rank]
+    v, i = cdist.sharded_select_mc_chunks(mine, q, job=_OracleChunkJob(q), merge_records=_oracle_merge_records)
+    out[rank] = (v.numpy().tolist(), i.numpy().tolist())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,chunk,q", [(2, 9000, 1000, 10), (3, 2500, 1000, 16), (3, 2000, 1000, 10)])
+def test_sharded_chunks_equal_global(world, N, chunk, q):
+    """Pools larger than HBM over several GPUs: chunk c streams on rank
+    c % world into that rank's running list; one all-gather of the running
+    lists + a merge equals the global selection (a rank may get no chunk)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_chunks, args=(world, _free_port(), N, chunk, q, 11, out), nprocs=world, join=True)
+    vg, ig = O.oracle_select_mc(_pool(N, 11), q, layout="NMC")
+    for r in range(world):
+        v, i = out[r]
+        assert list(i)[:len(ig)] == ig.tolist()

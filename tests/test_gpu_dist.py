@@ -52,6 +52,10 @@ def test_rccl_record_exchange_world1():
         av, ai = cdist.allgather_topq(v2, i2, 10)
         v3, i3 = ops.topq_merge(av, ai, 10)
         assert np.array_equal(i3.cpu().numpy(), exp)
+        # pools larger than HBM: this rank's chunks -> running list -> RCCL all-gather -> merge
+        chunks = [(Pd[lo:lo + 40_000], lo) for lo in range(0, P.shape[0], 40_000)]
+        _, i4 = cdist.sharded_select_mc_chunks(chunks, 10)
+        assert np.array_equal(i4.cpu().numpy(), exp)
     finally:
         dist.destroy_process_group()
 
