@@ -1,0 +1,143 @@
+// ce_abi_batch.hip -- C-ABI (include/ce.h): the mix ([mc; hc] row stack) and
+// batched users in one launch.
+#include "ce_host.hpp"
+
+using namespace ce;
+
+#ifdef CE_PHASE_TIMING
+extern "C" int ce_debug_phase(uint64_t* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), (size_t)n * 6 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+// ---- fused mix ---------------------------------------------------------------
+extern "C" size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t q) {
+    return lists_bytes((int64_t)pool_blocks(N) + pool_blocks(N_h), q < 1 ? 1 : q);
+}
+
+extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                             int64_t sC, const double* hc, int64_t N_h, int64_t ld_hc, int32_t q, void* ws,
+                             size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int rc = check_comm(a);
+    if (rc) return rc;
+    rc = check_q(q);
+    if (rc) return rc;
+    if (N_h < 0 || (N_h > 0 && (!hc || ld_hc < C)) || !val_out || !idx_out)
+        return fail(CE_EINVAL, "bad hc table / outputs");
+    const int G1 = pool_blocks(N), G2 = pool_blocks(N_h);
+    if (!ws || ws_bytes < lists_bytes((int64_t)G1 + G2, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, (int64_t)G1 + G2, q);
+    if (small_enabled() && q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= 2 * kSmallBSWide &&
+        N_h <= 2 * kSmallBSWide && (C == 4 || C == 8)) {
+        // both segments in ONE block (k_select_small, two segments)
+        const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
+        bool launched = false;
+        rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            if constexpr (S::kC == 4 || S::kC == 8) {
+                constexpr int CC = S::kC;
+                if (vec_ok(t, CC))
+                    launch_small_mix(src, make_src<kF64, CC, true>(t), N, N_h, q, val_out, idx_out, st);
+                else
+                    launch_small_mix(src, make_src<kF64, CC, false>(t), N, N_h, q, val_out, idx_out, st);
+                launched = true;
+            }
+        });
+        if (rc == CE_OK && launched) return check_launch("ce_select_mix");
+    }
+    // both segments on the streaming engine when it applies (q <= 64): the hc
+    // table is a committee of M = 1 member ([N_h, 1, C] f64, row stride ld_hc)
+    if (!launch_stream(a, G1, q, 0, w, st)) {
+        Seg s1{nullptr, N, G1, 0};
+        rc = committee_partial(a, s1, G1, q, w, nullptr, nullptr, false, st);
+        if (rc) return dispatch_err(rc, a);
+    }
+    WsLists w2{w.c + (size_t)G1 * q};
+    const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
+    if (launch_stream(t, G2, q, N, w2, st)) {
+        finish_lists(w, 1, G1 + G2, q, val_out, idx_out, st);
+        return check_launch("ce_select_mix");
+    }
+    Seg s2{nullptr, N_h, G2, N};
+    switch (C) {
+#define CE_T(CC) case CC: launch_partial(TableSrc<CC>{hc, ld_hc}, s2, G2, q, w2, nullptr, nullptr, false, st); break;
+        CE_T(2) CE_T(3) CE_T(4) CE_T(8)
+#undef CE_T
+        default: return fail(CE_EUNSUPPORTED, "mix with C=%d has no kernel in this build", C);
+    }
+    finish_lists(w, 1, G1 + G2, q, val_out, idx_out, st);
+    return check_launch("ce_select_mix");
+}
+
+// ---- batched users -------------------------------------------------------------
+// blocks per user: ~1024 items per block (two iterations per wave of a
+// 4-wave block), at most ~4096 blocks in all.  Measured at 500 x 1608 items:
+// 512 items/block 33.2 us, 1024 31.4 us, 2048 (one block per user, no merge
+// launch) 31.0 us; 256 45 us.
+static int batched_bpu(int64_t total, int U) {
+    if (U < 1) return 1;
+    const int64_t avg = cdiv(total, U);
+    int64_t bpu = cdiv(avg, (int64_t)1024);
+    const int64_t cap = std::max<int64_t>(1, 4096 / U);
+    bpu = std::max<int64_t>(1, std::min(bpu, cap));
+    return (int)bpu;
+}
+
+extern "C" size_t ce_select_batched_workspace_bytes(int64_t total_items, int32_t U, int32_t q) {
+    if (U < 1) U = 1;
+    return lists_bytes((int64_t)batched_bpu(total_items, U) * U, q < 1 ? 1 : q);
+}
+
+extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items, int32_t M, int32_t C, int64_t sN,
+                                 int64_t sM, int64_t sC, const int64_t* offsets, int32_t U, int32_t q, void* ws,
+                                 size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    CommArgs a{p, (int)dt, total_items, M, C, sN, sM, sC};
+    int rc = check_comm(a);
+    if (rc) return rc;
+    rc = check_q(q);
+    if (rc) return rc;
+    if (U < 1 || !offsets || !val_out || !idx_out) return fail(CE_EINVAL, "bad batched arguments");
+    const int bpu = batched_bpu(total_items, U);
+    const int64_t nl = (int64_t)bpu * U;
+    if (!ws || ws_bytes < lists_bytes(nl, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, nl, q);
+    if (small_enabled() && q <= kStreamMaxQ) {
+        // one 512-thread block per user when the average user fits one sweep
+        // (k_select_small; a longer user streams inside its block)
+        bool launched = false;
+        rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            if (cdiv(total_items, U) <= (int64_t)kSmallBS * small_ipt<S>()) {
+                launch_small<S, kSmallBS>(src, U, offsets, 0, 0, q, val_out, idx_out, nullptr, st);
+                launched = true;
+            }
+        });
+        if (rc == CE_OK && launched) return check_launch("ce_select_batched");
+    }
+    if (stream_enabled() && q <= kStreamMaxQ) {
+        // bpu 4-wave blocks per user, then one wave per user merges its bpu lists
+        rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            with_seg_batching<S>([&](auto unr, auto ipl) {
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>),
+                                   dim3((unsigned)nl), dim3(bpu == 1 && U < 64 ? 64 * kSegWaves : 256), 0, st, src, offsets,
+                                   (int64_t)0, (int64_t)0, q, bpu, val_out, idx_out, w.c, (const uint32_t*)nullptr);
+            });
+        });
+        if (rc == CE_OK) {
+            if (bpu > 1)
+                hipLaunchKernelGGL((k_merge_wave<false>), dim3((U + 3) / 4), dim3(256), 0, st,
+                                   ListSrc<false>{w.c, nullptr, nullptr}, U, bpu, q, val_out, idx_out);
+            return check_launch("ce_select_batched");
+        }
+    }
+    Seg sg{offsets, total_items, bpu, 0};
+    const bool fin = bpu == 1;
+    rc = committee_partial(a, sg, (int)nl, q, w, val_out, idx_out, fin, st);
+    if (rc) return dispatch_err(rc, a);
+    if (!fin) finish_lists(w, U, bpu, q, val_out, idx_out, st);
+    return check_launch("ce_select_batched");
+}

@@ -1,0 +1,204 @@
+// ce_abi_select.hip -- C-ABI (include/ce.h): the fused mc selection (streaming
+// stage 1 + merge, single-block small pools), exclusion-bitmap selection, the
+// multi-GPU exchange records and chunked pools larger than HBM.
+#include "ce_host.hpp"
+
+using namespace ce;
+
+// ---- fused mc ----------------------------------------------------------------
+extern "C" size_t ce_select_mc_workspace_bytes(int64_t N, int32_t q) { return ce_topq_workspace_bytes(N, q); }
+
+static int mc_partial(const CommArgs& a, int q, int64_t base_idx, void* ws, size_t ws_bytes, double* val_out,
+                      int64_t* idx_out, bool allow_final, int* G_out, bool* final_out, hipStream_t st) {
+    int rc = check_comm(a);
+    if (rc) return rc;
+    rc = check_q(q);
+    if (rc) return rc;
+    const int G = pool_blocks(a.N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    WsLists w = carve(ws, G, q);
+    *G_out = G;
+    *final_out = false;
+    if (launch_stream(a, G, q, base_idx, w, st)) return CE_OK;
+    Seg sg{nullptr, a.N, G, base_idx};
+    const bool fin = allow_final && G == 1;
+    rc = committee_partial(a, sg, G, q, w, val_out, idx_out, fin, st);
+    if (rc) return dispatch_err(rc, a);
+    *final_out = fin;
+    return CE_OK;
+}
+
+static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                          int64_t sC, const uint32_t* excl, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes,
+                          double* val_out, int64_t* idx_out, ce_stream_t stream);
+
+extern "C" int ce_select_mc(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                            int64_t sC, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes, double* val_out,
+                            int64_t* idx_out, ce_stream_t stream) {
+    return select_mc_impl(p, dt, N, M, C, sN, sM, sC, nullptr, q, base_idx, ws, ws_bytes, val_out, idx_out, stream);
+}
+
+extern "C" size_t ce_excl_words(int64_t N) { return N > 0 ? (size_t)((N + 31) / 32) : 0; }
+
+extern "C" int ce_select_mc_excl(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                                 int64_t sM, int64_t sC, const uint32_t* excl, int32_t q, int64_t base_idx, void* ws,
+                                 size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    if (!excl && N > 0) return fail(CE_EINVAL, "null exclusion bitmap");
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "exclusion bitmaps need q <= %d (got %d)", kStreamMaxQ, q);
+    return select_mc_impl(p, dt, N, M, C, sN, sM, sC, excl, q, base_idx, ws, ws_bytes, val_out, idx_out, stream);
+}
+
+static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                          int64_t sC, const uint32_t* excl, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes,
+                          double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    if (!val_out || !idx_out) return fail(CE_EINVAL, "null output");
+    hipStream_t st = (hipStream_t)stream;
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int rc0 = check_comm(a);
+    if (rc0) return rc0;
+    rc0 = check_q(q);
+    if (rc0) return rc0;
+    // the workspace contract holds on every path, even the one that does not touch it
+    if (!ws || ws_bytes < lists_bytes(pool_blocks(N), q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (small_enabled() && q <= kStreamMaxQ && N > 0) {
+        // one block scores and selects the whole pool (k_select_small)
+        bool launched = false;
+        const int rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            if (N <= (int64_t)kSmallBS * small_ipt<S>()) {
+                launch_small<S, kSmallBS>(src, 1, nullptr, N, base_idx, q, val_out, idx_out, excl, st);
+                launched = true;
+            } else if (N <= (int64_t)kSmallBSWide * small_ipt<S>()) {
+                launch_small<S, kSmallBSWide>(src, 1, nullptr, N, base_idx, q, val_out, idx_out, excl, st);
+                launched = true;
+            }
+        });
+        if (rc == CE_OK && launched) return check_launch("ce_select_mc");
+    }
+    if (stream_enabled() && q <= kStreamMaxQ && N > 0 &&
+        N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes) {
+        // small pool: ~512 items per 4-wave block on a few CUs (one block: it
+        // is the final answer), then one wave merges the blocks' lists
+        const int nb = (int)std::min<int64_t>(std::min<int64_t>(cdiv(N, 512), 32), pool_blocks(N));
+        WsLists w = carve(ws, nb, q);
+        const int rc = with_committee(a, [&](auto src) {
+            using S = decltype(src);
+            with_seg_batching<S>([&](auto unr, auto ipl) {
+                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(nb),
+                                   dim3(256), 0, st, src, nullptr, N, base_idx, q, nb, val_out, idx_out, w.c, excl);
+            });
+        });
+        if (rc == CE_OK) {
+            if (nb > 1)
+                hipLaunchKernelGGL((k_merge_wave<false>), dim3(1), dim3(256), 0, st, ListSrc<false>{w.c, nullptr, nullptr},
+                                   1, nb, q, val_out, idx_out);
+            return check_launch("ce_select_mc");
+        }
+    }
+    int G = 0;
+    bool fin = false;
+    int rc;
+    if (excl) {  // the streaming engine only (the q > 64 paths take no bitmap)
+        G = pool_blocks(N);
+        if (!stream_enabled() || !wide2_enabled() || !launch_stream(a, G, q, base_idx, carve(ws, G, q), st, excl))
+            return fail(CE_EUNSUPPORTED, "exclusion bitmap: no streaming kernel for this shape");
+    } else {
+        rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, &fin, st);
+        if (rc) return rc;
+    }
+    if (!fin) finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
+    return check_launch("ce_select_mc");
+}
+
+extern "C" int ce_select_mc_partial(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                                    int64_t sM, int64_t sC, int32_t q, int64_t base_idx, void* ws,
+                                    size_t ws_bytes, ce_stream_t stream) {
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int G = 0;
+    bool fin = false;
+    int rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &G, &fin, (hipStream_t)stream);
+    if (rc) return rc;
+    return check_launch("ce_select_mc_partial");
+}
+
+extern "C" int ce_select_finish(int64_t N, int32_t q, void* ws, size_t ws_bytes, double* val_out, int64_t* idx_out,
+                                ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (N < 0 || !val_out || !idx_out) return fail(CE_EINVAL, "bad finish arguments");
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, (hipStream_t)stream);
+    return check_launch("ce_select_finish");
+}
+
+// ---- exchange records (multi-GPU) -------------------------------------------
+static_assert(sizeof(ce_cand) == sizeof(Cand) && alignof(ce_cand) <= alignof(Cand), "ce_cand must mirror Cand");
+
+extern "C" int ce_select_finish_cands(int64_t N, int32_t q, void* ws, size_t ws_bytes, ce_cand* out,
+                                      ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "candidate records need q <= %d (got %d)", kStreamMaxQ, q);
+    if (N < 0 || !out) return fail(CE_EINVAL, "bad finish arguments");
+    if ((uintptr_t)out % 16) return fail(CE_EINVAL, "ce_cand output must be 16-byte aligned");
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    ListSrc<false> ls{carve(ws, G, q).c, nullptr, nullptr};
+    launch_finish(ls, 1, G, q, nullptr, nullptr, (hipStream_t)stream, reinterpret_cast<Cand*>(out));
+    return check_launch("ce_select_finish_cands");
+}
+
+extern "C" int ce_merge_cands(const ce_cand* c, int32_t nlists, int32_t q, double* val_out, int64_t* idx_out,
+                              ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (nlists < 1 || !c || !val_out || !idx_out) return fail(CE_EINVAL, "bad merge arguments");
+    if ((uintptr_t)c % 16) return fail(CE_EINVAL, "ce_cand input must be 16-byte aligned");
+    ListSrc<false> ls{reinterpret_cast<const Cand*>(c), nullptr, nullptr};
+    launch_finish(ls, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
+    return check_launch("ce_merge_cands");
+}
+
+// ---- chunked pools (larger than HBM) ----------------------------------------
+__global__ void k_cand_empty(Cand* __restrict__ c, int q) {
+    for (int r = threadIdx.x; r < q; r += blockDim.x) c[r] = Cand{0ull, -1};
+}
+
+extern "C" size_t ce_select_mc_chunk_workspace_bytes(int64_t N, int32_t q) {
+    return lists_bytes((int64_t)pool_blocks(N) + 1, q < 1 ? 1 : q);
+}
+
+// Stage 1 on the chunk (its G block lists), then ONE merge of those G lists
+// plus the running list (copied to list slot G of the workspace) back into
+// `running`: the running list always holds the top-q of every chunk so far
+// (the top-q of a union is within the union of the parts' top-qs).
+extern "C" int ce_select_mc_chunk(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                                  int64_t sM, int64_t sC, int32_t q, int64_t base_idx, ce_cand* running,
+                                  int32_t first, void* ws, size_t ws_bytes, ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "chunked selection needs q <= %d (got %d)", kStreamMaxQ, q);
+    if (!running || (uintptr_t)running % 16) return fail(CE_EINVAL, "running list must be 16-byte aligned device memory");
+    if (N < 0 || base_idx < 0) return fail(CE_EINVAL, "bad chunk N=%lld base_idx=%lld", (long long)N, (long long)base_idx);
+    hipStream_t st = (hipStream_t)stream;
+    Cand* run = reinterpret_cast<Cand*>(running);
+    if (N == 0) {
+        if (first) hipLaunchKernelGGL(k_cand_empty, dim3(1), dim3(64), 0, st, run, q);
+        return check_launch("ce_select_mc_chunk");
+    }
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes((int64_t)G + 1, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    WsLists w = carve(ws, (int64_t)G + 1, q);
+    if (!first && hipMemcpyAsync(w.c + (int64_t)G * q, run, (size_t)q * sizeof(Cand), hipMemcpyDeviceToDevice, st) !=
+                      hipSuccess)
+        return fail(CE_ELAUNCH, "running-list copy failed");
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int Gs = 0;
+    bool fin = false;
+    rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &Gs, &fin, st);
+    if (rc) return rc;
+    launch_finish(ListSrc<false>{w.c, nullptr, nullptr}, 1, G + (first ? 0 : 1), q, nullptr, nullptr, st, run);
+    return check_launch("ce_select_mc_chunk");
+}
+

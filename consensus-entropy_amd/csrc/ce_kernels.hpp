@@ -1,0 +1,790 @@
+// ce_kernels.hpp -- MI355X (gfx950) kernel templates shared by the C-ABI translation units
+// (ce_abi_core.hip, ce_abi_select.hip, ce_abi_batch.hip).
+//
+// Kernels (DESIGN.md has the roofline of each):
+//   k_partial<Src>   score items (committee consensus entropy, an entropy
+//                    vector, or an hc table row) and keep a per-block top-q in
+//                    LDS; one pass over HBM, entropies never written back.
+//                    Replaces amg_test.py:441-445 / :451-452 / :479-480.
+//   k_finish         merge the blocks' (or ranks') candidate lists into the
+//                    final top-q; one block per segment (user / pool).
+//   k_entropy        per-item entropy to HBM (ce_committee_entropy).
+//   k_vote / k_va    hc frequency table + entropy from votes (amg_test.py:88-117).
+//   k_segment_mean   frame -> song mean of one member (groupby mean, amg_test.py:437).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdarg.h>
+
+#include <algorithm>
+#include <type_traits>
+#include <cstdlib>
+
+#include "../../include/ce.h"
+#include "ce_device.hpp"
+#include "ce_topq.hpp"
+#include "ce_wide.hpp"
+#include "ce_stream.hpp"
+#include "ce_members.hpp"
+#include "ce_abi.hpp"
+
+namespace ce {
+
+constexpr int kBS = 256;          // stage-1 block: 4 waves
+constexpr int kFinBS = 1024;      // stage-2 block: 16 waves
+constexpr int kMinItemsPerBlock = 64;
+constexpr int64_t kSmallPoolBytes = 256 * 1024;  // below this one block does the whole selection
+constexpr int kMaxBlocks = 1024;  // stage-1 blocks per pool (4 per CU on 256 CUs)
+constexpr int kSegWaves = 16;     // waves per single-block pool / per user (k_stream_seg)
+
+// ---------------------------------------------------------------------------
+// Item sources.  key(i) returns the order key of global item i.
+// ---------------------------------------------------------------------------
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+template <int DT, int C, bool VEC>
+struct CommitteeSrc {
+    const void* p;
+    int64_t sN, sM, sC;
+    int M;
+    double dM, invM;
+    bool pow2;
+    static constexpr int kC = C;
+    static constexpr int kDT = DT;
+    static constexpr int kUnr = DT == kF64 ? 4 : 8;
+    __device__ __forceinline__ void mean(int64_t i, double (&m)[C]) const {
+        committee_mean<DT, C, VEC, kUnr>(p, i * sN, M, sM, sC, dM, invM, pow2, m);
+    }
+    // IPL items at once: all their member loads in flight together
+    // hook() runs after the means, before the first log (e.g. LogTablePrefetch::commit)
+    template <int UNR, int IPL, class Hook = NoHook>
+    __device__ __forceinline__ void keys(const int64_t (&items)[IPL], uint64_t (&k)[IPL], Hook hook = {}) const {
+        int64_t offs[IPL];
+#pragma unroll
+        for (int u = 0; u < IPL; ++u) offs[u] = items[u] * sN;
+        double m[IPL][C];
+        committee_mean_multi<DT, C, VEC, UNR, IPL>(p, offs, M, sM, sC, dM, invM, pow2, m);
+        hook();
+#pragma unroll
+        for (int u = 0; u < IPL; ++u) k[u] = order_key(entropy_row<C>(m[u]));
+    }
+    // keys() for latency-bound single-block pools: when the whole committee
+    // fits one batch (M <= UNR) the loads are issued item by item and each
+    // item's mean + entropy runs as soon as ITS loads have landed, so only the
+    // last item's arithmetic trails the last load.  Items u >= nlive (wave-
+    // uniform: no lane of the wave owns a real item there) skip the arithmetic
+    // (key 0).  hook() as in keys().
+    template <int UNR, int IPL, class Hook = NoHook>
+    __device__ __forceinline__ void keys_small(const int64_t (&items)[IPL], uint64_t (&k)[IPL], int nlive,
+                                               Hook hook = {}) const {
+        if (M > UNR) {
+            keys<UNR, IPL>(items, k, hook);
+            return;
+        }
+        MemberLoad<DT, C, VEC> ld[IPL][UNR];
+#pragma unroll
+        for (int u = 0; u < IPL; ++u)
+#pragma unroll
+            for (int v = 0; v < UNR; ++v) ld[u][v].load(p, items[u] * sN + (int64_t)(v < M ? v : M - 1) * sM, sC);
+        hook();
+        auto item = [&](auto full) {
+#pragma unroll
+            for (int u = 0; u < IPL; ++u) {
+                k[u] = 0;
+                if (u >= nlive) continue;  // wave-uniform
+                double acc[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) acc[c] = 0.0;
+#pragma unroll
+                for (int v = 0; v < UNR; ++v) {
+                    if constexpr (decltype(full)::value) ld[u][v].add_to(acc);  // M == UNR: no padding
+                    else ld[u][v].add_masked(acc, v < M);
+                }
+                double m[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) m[c] = div_members(acc[c], dM, invM, pow2);
+                k[u] = order_key(entropy_row<C>(m));
+            }
+        };
+        if (M == UNR) item(std::true_type());
+        else item(std::false_type());
+    }
+    __device__ __forceinline__ double entropy(int64_t i) const {
+        double m[C];
+        mean(i, m);
+        return entropy_row<C>(m);
+    }
+    __device__ __forceinline__ uint64_t key(int64_t i) const { return order_key(entropy(i)); }
+};
+
+struct ArraySrc {  // precomputed entropies
+    const double* e;
+    __device__ __forceinline__ uint64_t key(int64_t i) const { return order_key(e[i]); }
+};
+
+template <int C>
+struct TableSrc {  // hc frequency table rows [N_h, C] f64 (amg_test.py:451)
+    const double* t;
+    int64_t ld;
+    __device__ __forceinline__ uint64_t key(int64_t i) const {
+        double row[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) row[c] = t[i * ld + c];
+        return order_key(entropy_row<C>(row));
+    }
+};
+
+// Segment geometry: block b -> segment b / bpu, chunk b % bpu.
+struct Seg {
+    const int64_t* offsets;  // [U+1] device, or nullptr: one segment [0, N)
+    int64_t N;
+    int bpu;
+    int64_t base_idx;
+};
+
+__device__ __forceinline__ void seg_range(const Seg& sg, int64_t& s0, int64_t& lo, int64_t& hi) {
+    const int b = blockIdx.x;
+    const int u = b / sg.bpu, c = b % sg.bpu;
+    int64_t s1;
+    if (sg.offsets) {
+        s0 = sg.offsets[u];
+        s1 = sg.offsets[u + 1];
+    } else {
+        s0 = 0;
+        s1 = sg.N;
+    }
+    const int64_t len = s1 > s0 ? s1 - s0 : 0;
+    int64_t per = (len + sg.bpu - 1) / sg.bpu;
+    per = (per + kBS - 1) / kBS * kBS;
+    lo = s0 + (int64_t)c * per;
+    hi = lo + per < s1 ? lo + per : s1;
+    if (lo > hi) lo = hi;
+}
+
+// Write a finished top-q: either (key, idx) candidates into the workspace, or
+// the final (val, idx) outputs.  Slots past `cnt` are padding (idx -1).
+template <int CAP, bool FINAL>
+__device__ __forceinline__ void write_list(const TopQSmem<CAP>& s, int cnt, int q, Cand* wc, double* oval,
+                                           int64_t* oidx) {
+    for (int r = threadIdx.x; r < q; r += blockDim.x) {
+        const bool ok = r < cnt;
+        if constexpr (FINAL) {
+            oval[r] = ok ? key_to_val(s.key[r]) : __longlong_as_double(0x7ff8000000000000ll);
+            oidx[r] = ok ? s.idx[r] : -1;
+        } else {
+            wc[r] = Cand{ok ? s.key[r] : 0ull, ok ? s.idx[r] : -1};
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1: score + per-block top-q.  One item per thread per round.
+// ---------------------------------------------------------------------------
+template <class Src, int CAP, bool FINAL>
+__global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, Cand* __restrict__ wc, double* __restrict__ oval,
+                                                 int64_t* __restrict__ oidx) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    __shared__ TopQSmem<CAP> sm;
+    TopQ<CAP, kBS> tq(sm);
+    tq.init();
+    int64_t s0, lo, hi;
+    seg_range(sg, s0, lo, hi);
+    const int64_t rel = sg.base_idx - s0;
+    for (int64_t i0 = lo; i0 < hi; i0 += kBS) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool valid = i < hi;
+        uint64_t k = 0;
+        if (valid) k = src.key(i);
+        tq.offer(k, i + rel, valid);
+        tq.end_round(q, kBS);
+    }
+    const int cnt = tq.finish(q);
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    write_list<CAP, FINAL>(sm, cnt, q, wc + slot, oval + (FINAL ? slot : 0), oidx + (FINAL ? slot : 0));
+}
+
+// Wide-class variant of k_partial (q > 64 / segments): a wave scores 64
+// consecutive items (one per lane slot), so a block round is still 256.
+template <int DT, int NPL, bool VEC, int CAP, bool FINAL>
+__global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q, Cand* __restrict__ wc,
+                                                      double* __restrict__ oval, int64_t* __restrict__ oidx);
+
+// Wide classes on the streaming engine (q <= 64): one wave per item, every
+// wave independent, per-wave top-q.  NPL = classes owned per lane (C <= 64*NPL).
+template <int DT, int NPL, bool VEC>
+__device__ __forceinline__ double wide_item(const WideArgs& a, const PwPlan& pl, int64_t it, double* row,
+                                            double* scratch) {
+    if constexpr (VEC) {
+        constexpr int KCH = NPL / ChunkT<DT>::CPC;
+        constexpr int UNR = KCH >= 8 ? 1 : 8 / KCH;
+        return wave_item_entropy_vec<DT, KCH, UNR>(a.p, it * a.sN, a.M, a.C, a.sM, a.dM, a.invM, a.pow2, pl, row,
+                                                   scratch);
+    } else {
+        return wave_item_entropy<DT, NPL>(a.p, it * a.sN, a.M, a.C, a.sM, a.sC, a.dM, a.invM, a.pow2, pl, row,
+                                          scratch, nullptr);
+    }
+}
+
+template <int DT, int NPL, bool VEC, int CAP, bool FINAL>
+__global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg sg, int q, Cand* __restrict__ wc,
+                                                      double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    __shared__ TopQSmem<CAP> sm;
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    TopQ<CAP, kBS> tq(sm);
+    tq.init();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    int64_t s0, lo, hi;
+    seg_range(sg, s0, lo, hi);
+    const int64_t rel = sg.base_idx - s0;
+    for (int64_t i0 = lo; i0 < hi; i0 += kBS) {
+        uint64_t mykey = 0;
+        const int64_t wbase = i0 + 64 * w;
+        for (int j = 0; j < 64; ++j) {
+            const int64_t it = wbase + j;
+            if (it >= hi) break;  // wave-uniform
+            const double h = wide_item<DT, NPL, VEC>(a, pl, it, row, scratch);
+            if (lane == j) mykey = order_key(h);
+        }
+        const int64_t i = i0 + threadIdx.x;
+        tq.offer(mykey, i + rel, i < hi);
+        tq.end_round(q, kBS);
+    }
+    const int cnt = tq.finish(q);
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    write_list<CAP, FINAL>(sm, cnt, q, wc + slot, oval + (FINAL ? slot : 0), oidx + (FINAL ? slot : 0));
+}
+
+template <int DT, int NPL, bool VEC>
+__global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, StreamArgs sa, int q,
+                                                     Cand* __restrict__ wc) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    __shared__ WaveLists sm;
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+    int64_t lo = gw * sa.per_wave;
+    int64_t hi = lo + sa.per_wave;
+    if (hi > a.N) hi = a.N;
+    if (lo > hi) lo = hi;
+    RegTopQ tq;
+    tq.init(q);
+    for (int64_t t0 = lo; t0 < hi; t0 += 64) {
+        uint64_t mykey = 0;
+        for (int j = 0; j < 64; ++j) {
+            const int64_t it = t0 + j;
+            if (it >= hi) break;  // wave-uniform
+            const double h = wide_item<DT, NPL, VEC>(a, pl, it, row, scratch);
+            if (lane == j) mykey = order_key(h);
+        }
+        const int64_t i = t0 + lane;
+        tq.offer(mykey, i + sa.base_idx, i < hi);
+    }
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
+}
+
+// Wide classes, vectorised rows (q <= 64): one wave per item, lanes over 16-B
+// chunks, software-pipelined over the wave's flat sequence of (item, member
+// batch) pairs -- batch t+1 is in flight while batch t is added, and the next
+// item's first batch while an item's entropy is computed, so the wave always
+// has 2 x UNR x KCH 16-B loads per lane outstanding.  Items per wave are not
+// rounded to 64 (a wide item is tens of KB): every wave of the resident grid
+// gets work.
+template <int DT, int KCH, int UNR>
+__global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
+                                                      Cand* __restrict__ wc) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    __shared__ WaveLists sm;
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+    int64_t lo = gw * sa.per_wave;
+    int64_t hi = lo + sa.per_wave;
+    if (hi > a.N) hi = a.N;
+    if (lo > hi) lo = hi;
+    RegTopQ tq;
+    tq.init(q);
+    const char* base = static_cast<const char*>(a.p);
+    const int64_t sNb = a.sN * EB, sMb = a.sM * EB;
+    const int K = a.C / CPC;
+    const int NB = a.M / UNR;  // UNR divides M (host)
+    double acc[KCH * CPC];
+#pragma unroll
+    for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
+    uint64_t mykey = 0;
+    // issue cursor (item, batch) and consume cursor
+    int64_t ii = lo, ci = lo;
+    int ib = 0, cb = 0;
+    uint32_t off[KCH];  // this lane's chunk offsets in a member row (clamped into the row)
+#pragma unroll
+    for (int kk = 0; kk < KCH; ++kk) {
+        const int ch = lane + 64 * kk;
+        off[kk] = 16u * (uint32_t)(ch < K ? ch : K - 1);
+    }
+    WideBatch<DT, KCH, UNR> A, B;
+    auto issue = [&](WideBatch<DT, KCH, UNR>& X) {
+        X.issue(base + ii * sNb, ib * UNR, sMb, off);
+        if (++ib == NB) {
+            ib = 0;
+            ++ii;
+        }
+    };
+    auto consume = [&](const WideBatch<DT, KCH, UNR>& X) {
+        X.add(acc);
+        if (++cb == NB) {  // item ci complete
+            cb = 0;
+            const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
+#pragma unroll
+            for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
+            const int j = (int)((ci - lo) & 63);
+            if (lane == j) mykey = order_key(h);
+            if (j == 63 || ci == hi - 1) {
+                const int64_t t0 = ci - j;
+                bool ok = lane <= j;
+                if (sa.excl) ok = ok && !excluded(sa.excl, t0 + (lane <= j ? lane : j));
+                tq.offer(mykey, t0 + lane + sa.base_idx, ok);
+                mykey = 0;
+            }
+            ++ci;
+        }
+    };
+    if (ii < hi) issue(A);
+    while (ci < hi) {
+        if (ii < hi) issue(B);
+        consume(A);
+        if (ci >= hi) break;
+        if (ii < hi) issue(A);
+        consume(B);
+    }
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
+}
+
+template <int DT, int NPL, bool VEC>
+__global__ __launch_bounds__(kBS) void k_wide_entropy_v(WideArgs a, PwPlan pl, double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
+    const int w = threadIdx.x >> 6;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < a.N; i += (int64_t)gridDim.x * 4) {
+        const double h = wide_item<DT, NPL, VEC>(a, pl, i, row, scratch);
+        if ((threadIdx.x & 63) == 0) ent[i] = h;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stage 2: merge `nl` lists of q slots (per segment = blockIdx.x) into top-q.
+// A list's worst entry bounds the answer from below: with T = the best of the
+// full lists' worst entries, at least q candidates are >= T, so only
+// candidates >= T can be selected -- the filter is exact and usually leaves
+// ~q survivors.
+// ---------------------------------------------------------------------------
+template <bool FROM_VALS>
+struct ListSrc {
+    const Cand* c;
+    const double* val;
+    const int64_t* idx;
+    __device__ __forceinline__ void get(int64_t j, uint64_t& k, int64_t& i) const {
+        if constexpr (FROM_VALS) {
+            i = idx[j];
+            k = order_key(val[j]);
+        } else {
+            const Cand x = c[j];
+            k = x.key;
+            i = x.idx;
+        }
+    }
+};
+
+__device__ __forceinline__ void wave_best(uint64_t& k, int64_t& i) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t k2 = __shfl_xor(k, off);
+        const int64_t i2 = __shfl_xor(i, off);
+        if (better(k2, i2, k, i)) {
+            k = k2;
+            i = i2;
+        }
+    }
+}
+
+template <bool FROM_VALS, int CAP, int BS, int IPT>
+__global__ __launch_bounds__(BS) void k_finish(ListSrc<FROM_VALS> src, int nl, int q,
+                                               double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    __shared__ TopQSmem<CAP> sm;
+    __shared__ uint64_t wk[BS / 64];
+    __shared__ int64_t wi[BS / 64];
+    const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
+    const int64_t L = (int64_t)nl * q;
+    // 1. T = best over FULL lists of the list's worst entry; lists are
+    //    best-first, so a list is full iff slot q-1 is used and that slot is
+    //    its worst entry: one load per list.
+    uint64_t tk = 0;
+    int64_t ti = INT64_MAX;  // "nothing": admits every candidate
+    for (int g = threadIdx.x; g < nl; g += BS) {
+        uint64_t k;
+        int64_t i;
+        src.get(seg0 + (int64_t)g * q + q - 1, k, i);
+        if (i >= 0 && better(k, i, tk, ti)) {
+            tk = k;
+            ti = i;
+        }
+    }
+    wave_best(tk, ti);
+    if (lane_id() == 0) {
+        wk[threadIdx.x >> 6] = tk;
+        wi[threadIdx.x >> 6] = ti;
+    }
+    __syncthreads();
+    tk = wk[0];
+    ti = wi[0];
+    for (int w = 1; w < BS / 64; ++w)
+        if (better(wk[w], wi[w], tk, ti)) {
+            tk = wk[w];
+            ti = wi[w];
+        }
+    // admit candidates >= T: strictly better than (T.key, T.idx + 1)
+    TopQ<CAP, BS> tq(sm);
+    tq.init(tk, ti == INT64_MAX ? INT64_MAX : ti + 1);
+    // 2. filter every candidate; IPT independent loads per thread in flight
+    //    (addresses clamped, never a branch around a load)
+    for (int64_t b0 = 0; b0 < L; b0 += (int64_t)BS * IPT) {
+        uint64_t k[IPT];
+        int64_t id[IPT];
+#pragma unroll
+        for (int u = 0; u < IPT; ++u) {
+            int64_t j = b0 + (int64_t)u * BS + threadIdx.x;
+            const bool in = j < L;
+            src.get(seg0 + (in ? j : L - 1), k[u], id[u]);
+            if (!in) id[u] = -1;
+        }
+#pragma unroll
+        for (int u = 0; u < IPT; ++u) {
+            if (b0 + (int64_t)u * BS >= L) break;  // block-uniform
+            tq.offer(k[u], id[u], id[u] >= 0);
+            tq.end_round(q, BS);
+        }
+    }
+    const int cnt = tq.finish(q);
+    write_list<CAP, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
+}
+
+// Stage 2 for q <= kHeadsMaxQ (the common case, q = 10).  The lists are
+// best-first, so list heads are each list's best entry; T1 = the q-th best
+// head is an exact lower bound (q distinct lists hold an entry >= T1) and a
+// tight one: the global top-q sit in ~q different lists, so only ~q
+// candidates survive the filter.  Cost: one 1024-entry bitonic sort of the
+// heads + one pass over the (prefetched) candidates + a tiny final sort.
+constexpr int kHeadsBS = 1024;
+constexpr int kHeadsMaxQ = 512;
+
+template <bool FROM_VALS, int IPT>
+__global__ __launch_bounds__(kHeadsBS) void k_finish_heads(ListSrc<FROM_VALS> src, int nl, int q,
+                                                           double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    __shared__ TopQSmem<2048> sm;
+    const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
+    const int64_t L = (int64_t)nl * q;
+    const int tid = threadIdx.x;
+    // prefetch this thread's first IPT candidates (clamped, unconditional)
+    uint64_t k[IPT];
+    int64_t id[IPT];
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) {
+        const int64_t j = (int64_t)u * kHeadsBS + tid;
+        src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);
+        if (j >= L) id[u] = -1;
+    }
+    // best head among this thread's lists (distinct threads -> distinct lists)
+    uint64_t hk = 0;
+    int64_t hi = INT64_MAX;
+    for (int g = tid; g < nl; g += kHeadsBS) {
+        uint64_t kk;
+        int64_t ii;
+        src.get(seg0 + (int64_t)g * q, kk, ii);
+        if (ii >= 0 && better(kk, ii, hk, hi)) {
+            hk = kk;
+            hi = ii;
+        }
+    }
+    TopQ<2048, kHeadsBS> tq(sm);
+    uint64_t tk = 0;
+    int64_t ti = INT64_MAX;
+    if (q <= kHeadsBS / 64) {
+        // q <= 16: each wave's best head (shuffle reduction) comes from a list
+        // of its own; the q-th best of those 16 is the bound.
+        wave_best(hk, hi);
+        const int w = tid >> 6;
+        if ((tid & 63) == 0) {
+            sm.key[w] = hk;
+            sm.idx[w] = hi;
+        }
+        __syncthreads();
+        if (tid < kHeadsBS / 64) {
+            int rank = 0;
+            for (int v = 0; v < kHeadsBS / 64; ++v) rank += better(sm.key[v], sm.idx[v], sm.key[tid], sm.idx[tid]);
+            if (rank == q - 1) {
+                sm.red[0] = sm.key[tid];
+                sm.red[1] = (uint64_t)sm.idx[tid];
+            }
+        }
+        __syncthreads();
+        const int64_t t1 = (int64_t)sm.red[1];
+        if (t1 != INT64_MAX) {  // >= q non-empty lists
+            tk = sm.red[0];
+            ti = t1 + 1;  // admit candidates >= T1
+        }
+    } else {
+        sm.key[tid] = hk;
+        sm.idx[tid] = hi;
+        tq.sort_buffer(kHeadsBS);  // barrier inside, before the first compare
+        __syncthreads();
+        if (q <= kHeadsBS && sm.idx[q - 1] != INT64_MAX) {
+            tk = sm.key[q - 1];
+            ti = sm.idx[q - 1] + 1;
+        }
+    }
+    __syncthreads();
+    tq.init(tk, ti);
+    for (int64_t b0 = 0; b0 < L; b0 += (int64_t)kHeadsBS * IPT) {
+        if (b0 > 0) {
+#pragma unroll
+            for (int u = 0; u < IPT; ++u) {
+                const int64_t j = b0 + (int64_t)u * kHeadsBS + tid;
+                src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);
+                if (j >= L) id[u] = -1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < IPT; ++u) {
+            if (b0 + (int64_t)u * kHeadsBS >= L) break;  // block-uniform
+            tq.offer(k[u], id[u], id[u] >= 0);
+            tq.end_round(q, kHeadsBS);
+        }
+    }
+    const int cnt = tq.finish(q);
+    write_list<2048, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
+}
+
+// Stage 2 for q <= 64.  The lists are best-first, so a list's head is its
+// best entry.  Phase 1: each of the 16 waves sorts the heads of its share of
+// the lists (one per lane) in registers; its q-th best head T_w is an exact
+// lower bound (q distinct lists have an entry >= T_w), and so is T = the best
+// T_w.  Phase 2: the waves stream all candidates (64 consecutive per wave per
+// step, PF steps in flight) through register top-q lists floored at T -- only
+// candidates >= T (~q of them) are ever inserted -- and the lists are
+// tree-merged.  Output: final (val, idx), or candidate records (wc) for an
+// exchange between ranks.
+template <bool FROM_VALS>
+__global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int nl, int q,
+                                                    double* __restrict__ oval, int64_t* __restrict__ oidx,
+                                                    Cand* __restrict__ ocand) {
+    __shared__ WaveListsT<16> sm;
+    __shared__ uint64_t bk[16];
+    __shared__ int64_t bi[16];
+    constexpr int PF = 10;  // 16 x 64 x 10: 1024 lists of q = 10 in one round of loads
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
+    const int64_t L = (int64_t)nl * q;
+    // the first round of candidate loads goes out before the head phase
+    uint64_t k[PF];
+    int64_t id[PF];
+    auto load_round = [&](int64_t c0) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int64_t j = c0 + (int64_t)u * 16 * 64 + lane;
+            src.get(seg0 + (j < L ? j : L - 1), k[u], id[u]);  // clamped: no branch around a load
+            if (j >= L) id[u] = -1;
+        }
+    };
+    load_round((int64_t)w * 64);
+    // phase 1: the head bound (only worth a sort when there are many lists)
+    uint64_t fk = 0;
+    int64_t fi = INT64_MAX;
+    if (nl > 64) {
+        RegTopQ hq;
+        hq.init(q);
+        for (int g0 = w * 64; g0 < nl; g0 += 16 * 64) {
+            const int g = g0 + lane;
+            uint64_t hk = 0;
+            int64_t hid = -1;
+            src.get(seg0 + (int64_t)(g < nl ? g : nl - 1) * q, hk, hid);
+            hq.offer(hk, hid, g < nl && hid >= 0);
+        }
+        const uint64_t qk = readlane64(hq.k, q - 1);
+        const int64_t qi = (int64_t)readlane64((uint64_t)hq.i, q - 1);
+        if (lane == 0) {
+            bk[w] = qk;
+            bi[w] = qi;
+        }
+        __syncthreads();
+        for (int v = 0; v < 16; ++v)
+            if (bi[v] != INT64_MAX && better(bk[v], bi[v], fk, fi)) {
+                fk = bk[v];
+                fi = bi[v];
+            }
+        if (fi != INT64_MAX) fi += 1;  // admit candidates >= T: strictly better than (T.key, T.idx + 1)
+    }
+    RegTopQ tq;
+    tq.init(q, fk, fi);
+    for (int64_t c0 = (int64_t)w * 64; c0 < L; c0 += (int64_t)16 * 64 * PF) {
+        if (c0 != (int64_t)w * 64) load_round(c0);
+#pragma unroll
+        for (int u = 0; u < PF; ++u) tq.offer(k[u], id[u], id[u] >= 0);
+    }
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    if (ocand)
+        block_merge_write<16>(tq, sm, q, ocand + slot, 0);
+    else
+        block_merge_write<16>(tq, sm, q, nullptr, 0, oval + slot, oidx + slot);
+}
+
+// Per-segment merge of a few lists (batched users: bpu lists of q each): one
+// wave per segment streams its nl*q candidates through a register top-q.
+template <bool FROM_VALS>
+__global__ __launch_bounds__(256) void k_merge_wave(ListSrc<FROM_VALS> src, int segs, int nl, int q,
+                                                    double* __restrict__ oval, int64_t* __restrict__ oidx) {
+    const int seg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (seg >= segs) return;  // wave-uniform; no block barrier below
+    const int64_t L = (int64_t)nl * q, seg0 = (int64_t)seg * L;
+    RegTopQ tq;
+    tq.init(q);
+    for (int64_t c0 = 0; c0 < L; c0 += 64) {
+        const int64_t j = c0 + lane;
+        uint64_t k;
+        int64_t id;
+        src.get(seg0 + (j < L ? j : L - 1), k, id);
+        tq.offer(k, id, j < L && id >= 0);
+    }
+    if (lane < q) {
+        const bool ok = tq.i != INT64_MAX;
+        oval[(int64_t)seg * q + lane] = ok ? key_to_val(tq.k) : __longlong_as_double(0x7ff8000000000000ll);
+        oidx[(int64_t)seg * q + lane] = ok ? tq.i : -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Per-item entropy to HBM.
+// ---------------------------------------------------------------------------
+template <class Src>
+__global__ __launch_bounds__(kBS) void k_entropy(Src src, int64_t N, double* __restrict__ mean_out,
+                                                 double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    constexpr int C = Src::kC;
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < N; i += (int64_t)gridDim.x * kBS) {
+        double mean[C];
+        src.mean(i, mean);
+        if (mean_out)
+#pragma unroll
+            for (int c = 0; c < C; ++c) mean_out[i * C + c] = mean[c];
+        ent[i] = entropy_row<C>(mean);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// hc tables: one wave per row (amg_test.py:109-117).
+// ---------------------------------------------------------------------------
+template <int C>
+__device__ __forceinline__ void finish_counts(int (&cnt)[C], int64_t n_row, double* freq_out,
+                                              double* ent) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cnt[c] += __shfl_xor(cnt[c], off);
+    if (lane_id() == 0) {
+        int n = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) n += cnt[c];
+        double f[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) f[c] = round3((double)cnt[c] / (double)n);
+        if (freq_out)
+#pragma unroll
+            for (int c = 0; c < C; ++c) freq_out[n_row * C + c] = f[c];
+        ent[n_row] = entropy_row<C>(f);
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(kBS) void k_vote(const int8_t* __restrict__ votes, int64_t N, int A, int64_t ld,
+                                              double* __restrict__ freq, double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    const int lane = lane_id();
+    for (int64_t n = (int64_t)blockIdx.x * (kBS / 64) + (threadIdx.x >> 6); n < N;
+         n += (int64_t)gridDim.x * (kBS / 64)) {
+        int cnt[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) cnt[c] = 0;
+        const int8_t* row = votes + n * ld;
+        for (int a = lane; a < A; a += 64) {
+            const int v = row[a];
+#pragma unroll
+            for (int c = 0; c < C; ++c) cnt[c] += (v == c);
+        }
+        finish_counts<C>(cnt, n, freq, ent);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Frame -> song segment mean: pd.DataFrame(y_probs, index=X_train.index)
+// .groupby(['s_id']).mean() (amg_test.py:437, :469) as pandas 1.1.5's
+// group_mean computes it (the reference pins pandas==1.1.5): values upcast to
+// f64, per (song, class) a sequential sum over the song's frames in row order
+// skipping NaN, divided by the non-NaN count (0 -> NaN); a float32 column is
+// cast back to float32 at the end (the result dtype follows the input).
+// One thread per (song, class); frames of song n are rows perm[off[n]..off[n+1])
+// (perm == nullptr: rows off[n]..off[n+1] themselves, already grouped).
+// ---------------------------------------------------------------------------
+template <int DT, int ODT>
+__global__ __launch_bounds__(kBS) void k_segment_mean(const void* __restrict__ frames, int64_t ld, int C,
+                                                      const int64_t* __restrict__ perm,
+                                                      const int64_t* __restrict__ offsets, int64_t N,
+                                                      void* __restrict__ out, int64_t ldo) {
+    const int64_t total = N * C;
+    for (int64_t t = (int64_t)blockIdx.x * kBS + threadIdx.x; t < total; t += (int64_t)gridDim.x * kBS) {
+        const int64_t n = t / C;
+        const int c = (int)(t - n * C);
+        const int64_t f0 = offsets[n], f1 = offsets[n + 1];
+        double sum = 0.0;
+        int64_t cnt = 0;
+        // batches of 8 frames: the 8 loads are issued together (clamped rows,
+        // no branch around a load), then added in row order
+        constexpr int B = 8;
+        for (int64_t fb = f0; fb < f1; fb += B) {
+            double v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const int64_t f = fb + u < f1 ? fb + u : f1 - 1;
+                const int64_t r = perm ? perm[f] : f;
+                if constexpr (DT == kF32)
+                    v[u] = (double)static_cast<const float*>(frames)[r * ld + c];
+                else
+                    v[u] = static_cast<const double*>(frames)[r * ld + c];
+            }
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (fb + u < f1 && v[u] == v[u]) {  // not NaN
+                    sum += v[u];
+                    ++cnt;
+                }
+        }
+        double m = cnt ? sum / (double)cnt : __longlong_as_double(0x7ff8000000000000ll);
+        if constexpr (DT == kF32) m = (double)(float)m;  // the float32 result column
+        if constexpr (ODT == kF32)
+            static_cast<float*>(out)[n * ldo + c] = (float)m;
+        else
+            static_cast<double*>(out)[n * ldo + c] = m;
+    }
+}
+
+}  // namespace ce
