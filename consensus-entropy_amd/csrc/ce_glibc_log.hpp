@@ -201,9 +201,11 @@ __host__ __device__ __forceinline__ double glibc_log_fast(double x, const LogEnt
     const double r2 = r * r;
     const double p = __builtin_fma(r2, __builtin_fma(r, A[4], A[3]), __builtin_fma(r, A[2], A[1]));
     const double y = __builtin_fma(r * r2, p, __builtin_fma(r2, A[0], lo)) + hi;
-    const bool near1 = ix - 0x3fee000000000000ull < 0x3ff1090000000000ull - 0x3fee000000000000ull;
-    const bool special = (hw >> 16) - 0x0010u >= 0x7ff0u - 0x0010u;
-    if (__builtin_expect(near1 || special, 0)) return glibc_log(x, tab);
+    // the common case in ONE unsigned range test on the high word: x normal,
+    // positive and below the near-1 window (1 - 2^-4 = 0x3fee0000'00000000,
+    // whose low word is 0) -- every entropy term p < 0.9375.  Everything else
+    // (near 1, above it, subnormal, zero, negative, inf, NaN) takes glibc_log.
+    if (__builtin_expect(hw - 0x00100000u >= 0x3fee0000u - 0x00100000u, 0)) return glibc_log(x, tab);
     return y;
 }
 

@@ -394,6 +394,7 @@ static inline bool launch_stream(const CommArgs& a, int G, int q, int64_t base_i
                 constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
                 // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
                 constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
+                // a 2-batch register ring (3 and 4 measured: 72.8 / 71.9 % vs 72.6 % at C5)
                 auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
                 const int grid = resident_grid(kern, lds, G);
                 stream_grid(sa, grid);

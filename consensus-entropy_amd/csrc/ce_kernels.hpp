@@ -87,9 +87,11 @@ struct CommitteeSrc {
         }
         MemberLoad<DT, C, VEC> ld[IPL][UNR];
 #pragma unroll
-        for (int u = 0; u < IPL; ++u)
+        for (int u = 0; u < IPL; ++u) {
+            if (u >= nlive) break;  // wave-uniform: no load for slots without a real item
 #pragma unroll
             for (int v = 0; v < UNR; ++v) ld[u][v].load(p, items[u] * sN + (int64_t)(v < M ? v : M - 1) * sM, sC);
+        }
         hook();
         auto item = [&](auto full) {
 #pragma unroll
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 // has 2 x UNR x KCH 16-B loads per lane outstanding.  Items per wave are not
 // rounded to 64 (a wide item is tens of KB): every wave of the resident grid
 // gets work.
-template <int DT, int KCH, int UNR>
+template <int DT, int KCH, int UNR, int NB = 2>
 __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     const char* base = static_cast<const char*>(a.p);
     const int64_t sNb = a.sN * EB, sMb = a.sM * EB;
     const int K = a.C / CPC;
-    const int NB = a.M / UNR;  // UNR divides M (host)
+    const int NBM = a.M / UNR;  // member batches per item (UNR divides M, host)
     double acc[KCH * CPC];
 #pragma unroll
     for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
@@ -332,17 +334,17 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
         const int ch = lane + 64 * kk;
         off[kk] = 16u * (uint32_t)(ch < K ? ch : K - 1);
     }
-    WideBatch<DT, KCH, UNR> A, B;
+    WideBatch<DT, KCH, UNR> buf[NB];  // ring: NB - 1 batches in flight while one is added
     auto issue = [&](WideBatch<DT, KCH, UNR>& X) {
         X.issue(base + ii * sNb, ib * UNR, sMb, off);
-        if (++ib == NB) {
+        if (++ib == NBM) {
             ib = 0;
             ++ii;
         }
     };
     auto consume = [&](const WideBatch<DT, KCH, UNR>& X) {
         X.add(acc);
-        if (++cb == NB) {  // item ci complete
+        if (++cb == NBM) {  // item ci complete
             cb = 0;
             const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
 #pragma unroll
@@ -359,13 +361,16 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
             ++ci;
         }
     };
-    if (ii < hi) issue(A);
+#pragma unroll
+    for (int b = 0; b < NB - 1; ++b)
+        if (ii < hi) issue(buf[b]);
     while (ci < hi) {
-        if (ii < hi) issue(B);
-        consume(A);
-        if (ci >= hi) break;
-        if (ii < hi) issue(A);
-        consume(B);
+#pragma unroll
+        for (int s = 0; s < NB; ++s) {  // compile-time ring slots: no register-array indexing
+            if (ii < hi) issue(buf[(s + NB - 1) % NB]);
+            consume(buf[s]);
+            if (ci >= hi) break;
+        }
     }
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
 }
