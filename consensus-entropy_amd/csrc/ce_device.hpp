@@ -43,11 +43,18 @@ __device__ __forceinline__ bool better(uint64_t ka, int64_t ia, uint64_t kb, int
 // Branch-free form: for x == 0 and x < 0 the product is replaced, so the
 // log of a non-positive argument never reaches the result.  log is glibc's
 // (ce_glibc_log.hpp): the calling kernel has run stage_log_table().
-__device__ __forceinline__ double entr(double x) {
+__device__ __forceinline__ double entr_general(double x) {
     double r = -x * dlog(x);
     r = (x == 0.0) ? 0.0 : r;
     r = (x < 0.0) ? -__builtin_inf() : r;
     return r;  // NaN input: x==0 and x<0 are false, r = -NaN*log(NaN) = NaN
+}
+// The common case (x normal in (0, 0.9375): every term of a row with more than
+// one non-negligible class) is one multiply on the straight-line log; zeros,
+// negatives, NaN, subnormals and x near 1 take entr_general -- same values.
+__device__ __forceinline__ double entr(double x) {
+    if (__builtin_expect(!glibc_log_common(x), 0)) return entr_general(x);
+    return -x * glibc_log_core(x, s_log_tab);
 }
 
 // ---------------------------------------------------------------------------

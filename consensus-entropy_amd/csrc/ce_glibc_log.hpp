@@ -106,7 +106,12 @@ struct LogEntry {
     double invc, logc;
 };
 
-#define CE_GLIBC_LOG_DEFINE_TABLE(QUAL, NAME) QUAL double NAME[256] = {CE_GLIBC_LOG_TAB};
+// entries 0..127: glibc's {invc, logc}; entry 128: {A[1], A[3]}, the two
+// polynomial coefficients the FMAs take as addends (kept next to the table so
+// the device reads them with one LDS broadcast instead of rebuilding them in
+// VGPRs for every log: gfx950's VOP3 reads at most one SGPR pair)
+#define CE_GLIBC_LOG_DEFINE_TABLE(QUAL, NAME) \
+    QUAL double NAME[258] = {CE_GLIBC_LOG_TAB, 0x1.555555551305bp-2, 0x1.999b324f10111p-3};
 CE_GLIBC_LOG_DEFINE_TABLE(__device__ const, g_log_tab)
 CE_GLIBC_LOG_DEFINE_TABLE(static const, h_log_tab)
 
@@ -182,7 +187,15 @@ __host__ __device__ __forceinline__ double glibc_log(double x, const LogEntry* t
 // f64 FMA code; the near-1 window and the special inputs take glibc_log()
 // above under a branch the whole wave usually skips.  Same bits as glibc_log
 // for every input (the common-case operations are glibc_log's own).
-__host__ __device__ __forceinline__ double glibc_log_fast(double x, const LogEntry* tab) {
+// The common case only: x normal, positive and below the near-1 window
+// (1 - 2^-4 = 0x3fee0000'00000000, whose low word is 0) -- every entropy term
+// p < 0.9375.  Straight-line 32-bit integer + f64 FMA code, glibc_log's own
+// operations for that case.
+__host__ __device__ __forceinline__ bool glibc_log_common(double x) {
+    return (uint32_t)(dbits(x) >> 32) - 0x00100000u < 0x3fee0000u - 0x00100000u;
+}
+
+__host__ __device__ __forceinline__ double glibc_log_core(double x, const LogEntry* tab) {
     constexpr double A[5] = {CE_GLIBC_LOG_A};
     constexpr double Ln2[2] = {CE_GLIBC_LOG_LN2};
     const uint64_t ix = dbits(x);
@@ -199,22 +212,26 @@ __host__ __device__ __forceinline__ double glibc_log_fast(double x, const LogEnt
     const double hi = w + r;
     const double lo = __builtin_fma(kd, Ln2[1], w - hi + r);
     const double r2 = r * r;
-    const double p = __builtin_fma(r2, __builtin_fma(r, A[4], A[3]), __builtin_fma(r, A[2], A[1]));
-    const double y = __builtin_fma(r * r2, p, __builtin_fma(r2, A[0], lo)) + hi;
-    // the common case in ONE unsigned range test on the high word: x normal,
-    // positive and below the near-1 window (1 - 2^-4 = 0x3fee0000'00000000,
-    // whose low word is 0) -- every entropy term p < 0.9375.  Everything else
-    // (near 1, above it, subnormal, zero, negative, inf, NaN) takes glibc_log.
-    if (__builtin_expect(hw - 0x00100000u >= 0x3fee0000u - 0x00100000u, 0)) return glibc_log(x, tab);
-    return y;
+    const LogEntry a13 = tab[128];  // {A[1], A[3]}
+    const double p = __builtin_fma(r2, __builtin_fma(r, A[4], a13.logc), __builtin_fma(r, A[2], a13.invc));
+    return __builtin_fma(r * r2, p, __builtin_fma(r2, A[0], lo)) + hi;
+}
+
+// The same function as glibc_log for every input, laid out for the device:
+// the common case straight-line, everything else (near 1, above it,
+// subnormal, zero, negative, inf, NaN) through glibc_log under a branch the
+// wave usually skips.
+__host__ __device__ __forceinline__ double glibc_log_fast(double x, const LogEntry* tab) {
+    if (__builtin_expect(!glibc_log_common(x), 0)) return glibc_log(x, tab);
+    return glibc_log_core(x, tab);
 }
 
 // The block's LDS copy of the table (every kernel that computes an entropy
 // calls stage_log_table() at its top, before any early exit).
-__shared__ __attribute__((aligned(16))) LogEntry s_log_tab[128];
+__shared__ __attribute__((aligned(16))) LogEntry s_log_tab[129];
 
 __device__ __forceinline__ const LogEntry* stage_log_table() {
-    for (int j = threadIdx.x; j < 128; j += blockDim.x)
+    for (int j = threadIdx.x; j < 129; j += blockDim.x)
         s_log_tab[j] = LogEntry{g_log_tab[2 * j], g_log_tab[2 * j + 1]};
     __syncthreads();
     return s_log_tab;
@@ -224,16 +241,16 @@ __device__ __forceinline__ double dlog(double x) { return glibc_log_fast(x, s_lo
 // Split staging for latency-bound kernels: fetch() issues the table loads at
 // kernel start (before the data loads), commit() -- once the data has been
 // waited for anyway -- writes them to LDS and syncs the block (block-uniform).
-// Needs blockDim.x >= 128.
+// Needs blockDim.x >= 129.
 struct LogTablePrefetch {
     double invc, logc;
     __device__ __forceinline__ void fetch() {
-        const int j = threadIdx.x < 128 ? threadIdx.x : 127;
+        const int j = threadIdx.x < 129 ? threadIdx.x : 128;
         invc = g_log_tab[2 * j];
         logc = g_log_tab[2 * j + 1];
     }
     __device__ __forceinline__ void commit() const {
-        if (threadIdx.x < 128) s_log_tab[threadIdx.x] = LogEntry{invc, logc};
+        if (threadIdx.x < 129) s_log_tab[threadIdx.x] = LogEntry{invc, logc};
         __syncthreads();
     }
 };

@@ -632,7 +632,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     double* __restrict__ oval, int64_t* __restrict__ oidx, const uint32_t* __restrict__ excl) {
     constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
     constexpr int K = IPTA + IPTB, IB = IPTB > 0 ? IPTB : 1;
-    static_assert(BS % 64 == 0 && BS >= 128 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
+    static_assert(BS % 64 == 0 && BS >= 256 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
     using SM = SmallSmem<W>;
     __shared__ SM sm;
     CE_STAMP(blockIdx.x, 0)
