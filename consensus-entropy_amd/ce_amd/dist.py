@@ -15,6 +15,11 @@ send buffer and merged from the receive buffer as is (no pack/unpack kernels).
 The local-select and merge steps are injectable so the collective logic can be
 exercised on CPU with the gloo backend (tests/test_dist.py); by default they
 are the HIP operators.
+
+The other sharded configs of SURVEY.md §8(e): the mix stack [mc; hc] sharded
+over its concatenated index space (sharded_select_mix), batched users sharded
+over ranks with only a final gather (sharded_select_batched), and pools larger
+than HBM streamed per rank (sharded_select_mc_chunks).
 """
 from __future__ import annotations
 
@@ -106,6 +111,75 @@ def sharded_select_mc(P_local, q, *, global_offset, layout="NMC", group=None, lo
         return vals, idx
     all_vals, all_idx = allgather_topq(vals, idx, q, group)
     return merge(all_vals, all_idx, q)
+
+
+def sharded_select_mix(P_local, hc_local, q, *, n_items, item_offset, row_offset, layout="MNC", group=None,
+                       local_select=None, merge=None):
+    """The mix of amg_test.py:473-480 with the row stack [mc (N items); hc
+    (N_h rows)] sharded over ranks ("mix shards the
+    concatenated index space"): this rank holds committee items
+    [item_offset, +n) and hc rows [row_offset, +n_h).  Its two local top-q
+    lists carry global stack positions (item i -> i, row j -> n_items + j),
+    ONE all-gather moves 2q (entropy, position) pairs per rank, and the merge
+    over the 2*world lists equals ops.select_mix on the whole stack.
+
+    local_select  f(P, q, base_idx) -> (vals [q], idx [q]) for a committee
+                  (the hc rows are passed as a one-member f64 committee
+                  [1, n_h, C], "MNC"); default the fused HIP kernel
+    merge         f(vals, idx, q) -> (vals, idx); default ops.topq_merge
+    """
+    if local_select is None:
+        def local_select(P, qq, base, lay=layout):
+            return ops.select_mc(P, qq, lay, base_idx=base)
+    if merge is None:
+        merge = ops.topq_merge
+    v_mc, i_mc = local_select(P_local, q, int(item_offset))
+    hc1 = hc_local.to(torch.float64).unsqueeze(0)  # M = 1: the hc rows' entropy (amg_test.py:479)
+    v_hc, i_hc = local_select(hc1, q, int(n_items) + int(row_offset), "MNC")
+    vals, idx = torch.cat([v_mc, v_hc]), torch.cat([i_mc, i_hc])
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        vals, idx = allgather_topq(vals, idx, 2 * q, group)
+    return merge(vals, idx, q)
+
+
+def sharded_select_batched(P_local, offsets_local, q, *, n_users, layout="MNC", group=None, local_select=None):
+    """Batched users (BASELINE configs[2], the per-user loop of amg_test.py:345)
+    sharded over ranks with no collective but the final gather (SURVEY.md
+    §8(e)): rank r holds users shard_range(n_users, r, world) -- their items
+    in P_local, user u's at offsets_local[u]:offsets_local[u+1] -- selects
+    them in one launch, and ONE all-gather of the padded [ceil(U/world), q]
+    (entropy, position) blocks gives every rank the full (vals [U, q],
+    idx [U, q]), user-local positions, as one select_batched over all users.
+
+    local_select  f(P, offsets, q) -> (vals [U_r, q], idx [U_r, q]); default
+                  ops.select_batched (HIP)
+    """
+    if local_select is None:
+        def local_select(P, off, qq):
+            return ops.select_batched(P, off, qq, layout)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    lo, hi = shard_range(n_users, rank, world)
+    if offsets_local.numel() != hi - lo + 1:
+        raise ValueError(f"rank {rank} holds users [{lo}, {hi}): offsets_local needs {hi - lo + 1} entries")
+    if hi > lo:
+        vals, idx = local_select(P_local, offsets_local, q)
+    else:  # more ranks than users
+        vals = torch.empty((0, q), dtype=torch.float64, device=offsets_local.device)
+        idx = torch.empty((0, q), dtype=torch.int64, device=offsets_local.device)
+    if world == 1:
+        return vals, idx
+    umax = -(-int(n_users) // world)
+    send = torch.zeros((umax, 2 * q), dtype=torch.int64, device=vals.device)
+    send[:hi - lo, :q] = vals.contiguous().view(torch.int64)
+    send[:hi - lo, q:] = idx
+    recv = torch.empty((world * umax, 2 * q), dtype=torch.int64, device=vals.device)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    spans = [shard_range(n_users, r, world) for r in range(world)]
+    rows = torch.cat([torch.arange(r * umax, r * umax + (b - a), device=vals.device)
+                      for r, (a, b) in enumerate(spans)])
+    out = recv.index_select(0, rows)
+    return out[:, :q].contiguous().view(torch.float64), out[:, q:].contiguous()
 
 
 def sharded_select_mc_chunks(chunks, q, *, layout="NMC", group=None, job=None, merge_records=None):

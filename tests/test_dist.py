@@ -229,3 +229,112 @@ def test_sharded_chunks_equal_global(world, N, chunk, q):
     for r in range(world):
         v, i = out[r]
         assert list(i)[:len(ig)] == ig.tolist()
+
+
+def _mix_inputs(N, Nh, seed):
+    rng = np.random.default_rng(seed)
+    e = -np.log(rng.random((4, N, 4)))
+    P = e / e.sum(-1, keepdims=True)
+    P[:, ::7] = np.floor(P[:, ::7] * 8) / 8  # exact ties inside and across shards
+    votes = rng.integers(0, 4, size=(Nh, 12))
+    hc = np.stack([np.round((votes == c).sum(1) / 12, 3) for c in range(4)], 1)  # tie-heavy, amg_test.py:115
+    return P, hc
+
+
+def _oracle_local_any(P, q, base, layout="MNC"):
+    v, i = O.oracle_select_mc(P.numpy(), q, layout=layout)
+    vals = np.full(q, np.nan)
+    idx = np.full(q, -1, np.int64)
+    vals[:len(v)] = v
+    idx[:len(i)] = i + base
+    return torch.from_numpy(vals), torch.from_numpy(idx)
+
+
+def _worker_mix(rank, world, port, N, Nh, q, seed, out):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "consensus-entropy_amd"))
+    from ce_amd import dist as cdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P, hc = _mix_inputs(N, Nh, seed)
+    lo, hi = cdist.shard_range(N, rank, world)
+    lh, hh = cdist.shard_range(Nh, rank, world)
+    v, i = cdist.sharded_select_mix(torch.from_numpy(P[:, lo:hi]), torch.from_numpy(hc[lh:hh]), q, n_items=N,
+                                    item_offset=lo, row_offset=lh, local_select=_oracle_local_any,
+                                    merge=_oracle_merge)
+    out[rank] = i.numpy().tolist()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,Nh,q", [(2, 1608, 1608, 10), (3, 500, 97, 16), (2, 5, 3, 10)])
+def test_sharded_mix_equals_global(world, N, Nh, q):
+    """mix (amg_test.py:473-480) sharded over the concatenated [mc; hc] index
+    space: the merged answer is the single-process mix, hc positions >= N."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_mix, args=(world, _free_port(), N, Nh, q, 5, out), nprocs=world, join=True)
+    P, hc = _mix_inputs(N, Nh, 5)
+    _, ig = O.oracle_select_mix(P, hc, q)
+    for r in range(world):
+        got = out[r]
+        assert got[:len(ig)] == ig.tolist()
+        assert all(x == -1 for x in got[len(ig):])
+
+
+def _batched_inputs(U, seed):
+    rng = np.random.default_rng(seed)
+    n = rng.integers(1, 300, size=U)
+    n[0] = 11
+    offs = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+    e = -np.log(rng.random((4, int(offs[-1]), 4)))
+    P = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+    P[:, ::9] = np.floor(P[:, ::9] * 4) / 4
+    return P, offs
+
+
+def _oracle_batched(P, offs, q):
+    Pn, o = P.numpy(), offs.numpy()
+    vals = np.full((len(o) - 1, q), np.nan)
+    idx = np.full((len(o) - 1, q), -1, np.int64)
+    for u in range(len(o) - 1):
+        v, i = O.oracle_select_mc(np.ascontiguousarray(Pn[:, o[u]:o[u + 1]]), q)
+        vals[u, :len(v)] = v
+        idx[u, :len(i)] = i
+    return torch.from_numpy(vals), torch.from_numpy(idx)
+
+
+def _worker_batched(rank, world, port, U, q, seed, out):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "consensus-entropy_amd"))
+    from ce_amd import dist as cdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P, offs = _batched_inputs(U, seed)
+    ulo, uhi = cdist.shard_range(U, rank, world)
+    a, b = offs[ulo], offs[uhi]
+    v, i = cdist.sharded_select_batched(torch.from_numpy(np.ascontiguousarray(P[:, a:b])),
+                                        torch.from_numpy(offs[ulo:uhi + 1] - a), q, n_users=U,
+                                        local_select=_oracle_batched)
+    out[rank] = (v.numpy().tolist(), i.numpy().tolist())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,U,q", [(2, 37, 10), (3, 8, 5), (3, 2, 10)])
+def test_sharded_batched_equals_global(world, U, q):
+    """Batched users sharded over ranks, one final gather: every rank holds
+    the [U, q] answer of one launch over all users (a rank may hold none)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_batched, args=(world, _free_port(), U, q, 3, out), nprocs=world, join=True)
+    P, offs = _batched_inputs(U, 3)
+    vg, ig = _oracle_batched(torch.from_numpy(P), torch.from_numpy(offs), q)
+    for r in range(world):
+        v, i = out[r]
+        assert np.array_equal(np.array(i), ig.numpy())
+        assert np.array_equal(np.array(v), vg.numpy(), equal_nan=True)

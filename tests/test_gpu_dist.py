@@ -86,3 +86,46 @@ def test_bench_contract_small():
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] in ("port", "reference")
     assert len(line["selected"]) == 10
+
+
+def test_rccl_sharded_mix_and_batched_world1():
+    """sharded_select_mix / sharded_select_batched through the HIP kernels and
+    an RCCL world-1 group: equal to ops.select_mix / ops.select_batched and
+    to the oracle (the N > 1 exchange is covered on gloo)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import torch.distributed as dist
+
+    import ce_amd
+    from ce_amd import dist as cdist
+    from ce_amd import ops
+    from oracle import ce_oracle as O
+
+    ce_amd.load()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(8)
+        e = -np.log(rng.random((4, 1608, 4)))
+        P = e / e.sum(-1, keepdims=True)
+        P[:, ::5] = np.floor(P[:, ::5] * 8) / 8
+        votes = rng.integers(0, 4, size=(1608, 20))
+        hc = np.stack([np.round((votes == c).sum(1) / 20, 3) for c in range(4)], 1)
+        Pd, hd = torch.from_numpy(P).cuda(), torch.from_numpy(hc).cuda()
+        _, i1 = cdist.sharded_select_mix(Pd, hd, 10, n_items=1608, item_offset=0, row_offset=0)
+        _, i2 = ops.select_mix(Pd, hd, 10)
+        exp = O.oracle_select_mix(P, hc, 10)[1]
+        assert np.array_equal(i1.cpu().numpy(), exp) and np.array_equal(i2.cpu().numpy(), exp)
+        n = rng.integers(100, 1608, size=40)
+        offs = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+        e = -np.log(rng.random((4, int(offs[-1]), 4)))
+        Pb = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+        Pbd, od = torch.from_numpy(Pb).cuda(), torch.from_numpy(offs).cuda()
+        v3, i3 = cdist.sharded_select_batched(Pbd, od, 10, n_users=40)
+        v4, i4 = ops.select_batched(Pbd, od, 10)
+        assert torch.equal(i3, i4) and torch.equal(v3.view(torch.int64), v4.view(torch.int64))
+        for u in range(40):
+            eu = O.oracle_select_mc(np.ascontiguousarray(Pb[:, offs[u]:offs[u + 1]]), 10)[1]
+            assert np.array_equal(i3[u].cpu().numpy(), eu)
+    finally:
+        dist.destroy_process_group()
