@@ -216,6 +216,153 @@ __global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
     }
 }
 
+// GaussianNB for the reference's shape (D = 260 features, KC = C classes),
+// feature-streamed: k_gnb_proba8 holds a frame group's 33 feature values AND
+// one class's 33 terms in registers before each pairwise sum, and issues the
+// next group's loads only when the group is done.  Here the column loop is
+// outermost: x[m] feeds the KC classes' terms at once, and each term goes
+// straight into its numpy accumulator -- the pairwise plan of n = 260 is three
+// leaves, [0,128) [128,192) [192,260), so lane j's chain of leaf l is a running
+// sum over the columns of that leaf (first term assigned, then +=, as numpy's
+// r[j]) -- and the register x[m] is refilled with the NEXT group's value as
+// soon as it is consumed, so a whole group's loads are in flight during the
+// current group's arithmetic.  Per leaf the 8 chains are combined by the xor
+// butterfly (((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) in every lane of the group),
+// the 4 tail features 256..259 are added in order, and the row sum is
+// 0.0 + (L0 + (L1 + L2)) -- the same operations in the same order as
+// k_gnb_proba8 and numpy.  LDS: {theta, 1/var} pairs (one ds_read_b128) and
+// var, per class and feature.
+template <int KC, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gnb_stream260(GnbArgs a) {
+    constexpr int D = 260, NX = 33;
+    static_assert(pw_plan(D).nleaves == 3 && pw_plan(D).lstart[1] == 128 && pw_plan(D).lstart[2] == 192 &&
+                      pw_plan(D).llen[2] == 68,
+                  "the leaf layout this kernel hard-codes");
+    __shared__ __attribute__((aligned(16))) f64x2 tr[KC * D];  // {theta, RN(1/var)}
+    __shared__ double vr[KC * D];
+    __shared__ double hs1[KC];
+    for (int t = threadIdx.x; t < KC * D; t += blockDim.x) {
+        const double v = a.var[t];
+        tr[t] = f64x2{a.theta[t], 1.0 / v};
+        vr[t] = v;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, j = lane & 7, g = lane >> 3, w = threadIdx.x >> 6;
+    if (w == 0) {  // -0.5 * np.sum(np.log(2 pi var_c)): group c < KC computes class c
+        // leaf by leaf with rolled loops (one log live at a time; an unrolled
+        // 33-log body would set the whole kernel's register budget)
+        const int c = g < KC ? g : 0;
+        const double* v = vr + c * D + j;
+        auto lg = [&](int m) { return log(2. * M_PI * v[8 * m]); };
+        double L[3];
+        const int m0[3] = {0, 16, 24}, m1[3] = {16, 24, 32};
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            double r = lg(m0[l]);
+#pragma unroll 1
+            for (int m = m0[l] + 1; m < m1[l]; ++m) r += lg(m);
+            r = r + __shfl_xor(r, 1);
+            r = r + __shfl_xor(r, 2);
+            r = r + __shfl_xor(r, 4);
+            L[l] = r;
+        }
+        const double tl = j < 4 ? lg(32) : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) L[2] += __shfl(tl, (lane & ~7) + k);
+        const double s1 = 0.0 + (L[0] + (L[1] + L[2]));
+        if (g < KC && j == 0) hs1[g] = -0.5 * s1;
+    }
+    __syncthreads();
+    const int64_t step = (int64_t)gridDim.x * 32;
+    int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 8;
+    auto row_of = [&](int64_t fb) { const int64_t fr = fb + g; return a.X + (fr < a.F ? fr : a.F - 1) * a.ld; };
+    double x[NX];
+    {
+        const double* xr = row_of(f0);
+#pragma unroll
+        for (int m = 0; m < NX; ++m) x[m] = (m < NX - 1 || j < 4) ? __builtin_nontemporal_load(xr + 8 * m + j) : 0.0;
+    }
+    for (; f0 < a.F; f0 += step) {
+        const double* xn = row_of(f0 + step);  // next group (clamped: always a valid row)
+        // the table reads are loop-invariant: left visible, LICM hoists all 33 x KC
+        // of them out of the frame loop (hundreds of VGPRs, spills); an opaque
+        // per-iteration base keeps them in their column
+        int jo = j;
+        asm volatile("" : "+v"(jo));
+        double r[KC][3], tl[KC];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) {
+            const bool live = m < NX - 1 || j < 4;  // column 32: features 256..259 only
+            const double xm = x[m];
+            if (live) x[m] = __builtin_nontemporal_load(xn + 8 * m + j);
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                const int fc = live ? c * D + 8 * m + jo : c * D;
+                const f64x2 p = tr[fc];
+                const double d = xm - p.x;
+                const double t = live ? div_by_recip(d * d, vr[fc], p.y) : 0.0;
+                if (m == 0 || m == 16 || m == 24) r[c][m == 0 ? 0 : (m == 16 ? 1 : 2)] = t;
+                else if (m < 16) r[c][0] += t;
+                else if (m < 24) r[c][1] += t;
+                else if (m < 32) r[c][2] += t;
+                else tl[c] = t;
+                if constexpr (WPE >= 4) asm volatile("" ::: "memory");  // 4 waves: one class's table reads at a time
+            }
+            // pin each column's terms to their column: unconstrained, the compiler
+            // issues all 33 columns' table reads first and sinks every term after
+            // them (hundreds of live VGPRs, spills)
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+                if (m < 16) asm volatile("" : "+v"(r[c][0]));
+                else if (m < 24) asm volatile("" : "+v"(r[c][1]));
+                else if (m < 32) asm volatile("" : "+v"(r[c][2]));
+                else asm volatile("" : "+v"(tl[c]));
+            }
+            asm volatile("" ::: "memory");  // and the column's loads (the refill included) to their column
+        }
+        double jll[KC];
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+            double L[3];
+#pragma unroll
+            for (int l = 0; l < 3; ++l) {
+                double v = r[c][l];
+                v = v + __shfl_xor(v, 1);
+                v = v + __shfl_xor(v, 2);
+                v = v + __shfl_xor(v, 4);
+                L[l] = v;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) L[2] += __shfl(tl[c], (lane & ~7) + k);
+            const double s2 = 0.0 + (L[0] + (L[1] + L[2]));
+            double n_ij = hs1[c];
+            n_ij -= 0.5 * s2;
+            jll[c] = a.log_prior[c] + n_ij;
+        }
+        double mx = jll[0];
+#pragma unroll
+        for (int c = 1; c < KC; ++c) mx = jll[c] > mx ? jll[c] : mx;
+        if (!__builtin_isfinite(mx)) mx = 0.0;
+        // one transcendental at a time (the next group's 33 features are live
+        // here; overlapped exps would set the kernel's register peak)
+        double s = -0.0;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+            s += exp(jll[c] - mx);
+            asm volatile("" : "+v"(s));
+        }
+        const double lse = log(0.0 + s) + mx;
+        const int64_t fr = f0 + g;
+        if (fr < a.F && j < a.C) {
+            double jl = jll[0];
+#pragma unroll
+            for (int c = 1; c < KC; ++c)
+                if (c == j) jl = jll[c];
+            a.out[fr * a.ldo + j] = exp(jl - lse);  // lane j's class only: exp(jll[j] - lse)
+        }
+    }
+}
+
 // Lane j's partial dot product -> the group's d (butterfly) -> expit(d + b).
 __device__ __forceinline__ double sgd_expit(double d, double b) {
     d = d + __shfl_xor(d, 1);

@@ -670,6 +670,34 @@ def test_sgd_span_kernel_matches_general(ce, F):
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
+@pytest.mark.parametrize("F", [1, 7, 33, 20_003])
+def test_gnb_stream_kernel_matches_general(ce, F):
+    """The feature-streamed GaussianNB kernel (k_gnb_stream260: D = ld = 260,
+    C = 4) against the 8-lane kernel, reached through a padded view (ld = 264):
+    the same terms, accumulators, butterflies and exp/log, so the same bits,
+    ragged frame counts included."""
+    from conftest import fitted_members
+
+    gnb, _, Xt = fitted_members(n_test=F)
+    Xd = dev(Xt)
+    Xpad = torch.zeros((F, 264), dtype=torch.float64, device="cuda")
+    Xpad[:, :260] = Xd
+    got = ce.ops.gnb_predict_proba(Xd, gnb.theta_, gnb.var_, gnb.class_prior_).cpu().numpy()
+    want = ce.ops.gnb_predict_proba(Xpad[:, :260], gnb.theta_, gnb.var_, gnb.class_prior_).cpu().numpy()
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    # an infinite feature and a NaN feature: the inf / NaN paths of the terms
+    Xt2 = Xt.copy()
+    Xt2[0, 3] = np.inf
+    if F > 1:
+        Xt2[F - 1, 259] = np.nan
+    Xpad[:, :260] = dev(Xt2)
+    got = ce.ops.gnb_predict_proba(dev(Xt2), gnb.theta_, gnb.var_, gnb.class_prior_).cpu().numpy()
+    want = ce.ops.gnb_predict_proba(Xpad[:, :260], gnb.theta_, gnb.var_, gnb.class_prior_).cpu().numpy()
+    nan = np.isnan(want)  # NaN rows: NaN in both (the sign of a NaN is not a value)
+    assert nan[0].all() and np.array_equal(np.isnan(got), nan)
+    assert np.array_equal(got[~nan].view(np.uint64), want[~nan].view(np.uint64))
+
+
 def test_frames_inference_to_selection(ce):
     """amg_test.py:426-445 with every step on the device: member inference over
     frames (GNB, SGD), per-song segment mean, stack with a song-level member,
