@@ -6,7 +6,13 @@ normalised like sigmoid outputs -- scipy.stats.entropy normalises the mean
 row), one seeded generator per chunk.  Reports the scoring time (HIP events
 around every chunk's call on its stream: stage 1 + the running merge) and the
 job's wall time including generation, as one JSON line.
-  python tools/bench_c5.py [--items 50000000] [--chunk 250000] [--q 10]"""
+  python tools/bench_c5.py [--items 50000000] [--chunk 250000] [--q 10]
+Several GPUs (BASELINE configs[4] at 1/2/4/8 GPUs, one process per GPU):
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_c5.py
+chunk c is generated and scored on rank c % N into that rank's running list;
+one all-gather of the N running lists (16-B ce_cand records, RCCL) and the same
+merge on every rank give the pool's top-q (ce_amd.dist).
+Times are the max over ranks; rank 0 prints the line."""
 import argparse
 import json
 import os
@@ -22,7 +28,7 @@ import ce_amd.ops as ops  # noqa: E402
 PEAK = 8000.0
 
 
-def run(items=50_000_000, chunk=250_000, members=32, classes=1000, q=10, log=True):
+def run(items=50_000_000, chunk=250_000, members=32, classes=1000, q=10, log=True, rank=0, world=1):
     M, C, Nc = members, classes, chunk
     bufs = [torch.empty((min(Nc, items), M, C), dtype=torch.bfloat16, device="cuda") for _ in range(2)]
     # warm-up (untimed): module load, workspace allocation, occupancy queries
@@ -33,30 +39,41 @@ def run(items=50_000_000, chunk=250_000, members=32, classes=1000, q=10, log=Tru
     nch = (items + Nc - 1) // Nc
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for c in range(nch):
+    for c in range(rank, nch, world):  # this rank's chunks (all of them at world 1)
         lo = c * Nc
         n = min(Nc, items - lo)
-        buf = bufs[c & 1][:n]
+        buf = bufs[(c // world) & 1][:n]
         buf.uniform_(0.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1987 * 100_003 + c))
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        job.add(buf)
+        job.add(buf, lo)
         e1.record()
         evs.append((e0, e1))
-        if log and c % 20 == 0:
-            print(f"chunk {c}/{nch}", file=sys.stderr, flush=True)
-    vals, idx = job.result()
+        if log and c % 20 == rank % 20:
+            print(f"[rank {rank}] chunk {c}/{nch}", file=sys.stderr, flush=True)
+    rec = job.running_records(torch.device("cuda", torch.cuda.current_device()))
+    if world > 1:
+        from ce_amd import dist as cdist
+
+        rec = cdist.allgather_cands(rec)  # one RCCL all-gather of every rank's q records
+    vals, idx = ops.merge_cands(rec, q)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     score_s = sum(e0.elapsed_time(e1) for e0, e1 in evs) * 1e-3
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([wall, score_s], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, score_s = t.tolist()
     nbytes = items * M * C * 2
     del bufs
     torch.cuda.empty_cache()
     return {
         "config": f"configs[4] wide-class job: {items} items x {M} x {C} bf16 ({nbytes / 1e12:.2f} TB), "
-                  f"{nch} device-generated chunks of {Nc}, running top-{q}",
-        "items": items, "chunks": nch, "score_s": score_s, "items_per_s": items / score_s,
-        "GB_per_s": nbytes / score_s / 1e9, "frac_hbm": nbytes / score_s / 1e9 / PEAK,
+                  f"{nch} device-generated chunks of {Nc}, running top-{q}, {world} GPU(s)",
+        "items": items, "chunks": nch, "n_gpus": world, "score_s": score_s, "items_per_s": items / score_s,
+        "GB_per_s": nbytes / score_s / 1e9, "frac_hbm": nbytes / score_s / 1e9 / PEAK / world,
         "wall_s_incl_generation": wall,
         "selected": idx.cpu().tolist(), "entropies": vals.cpu().tolist()}
 
@@ -69,7 +86,17 @@ def main():
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--q", type=int, default=10)
     a = ap.parse_args()
-    print(json.dumps(run(a.items, a.chunk, a.members, a.classes, a.q)), flush=True)
+    rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+    line = run(a.items, a.chunk, a.members, a.classes, a.q, rank=rank, world=world)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
