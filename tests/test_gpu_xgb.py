@@ -57,6 +57,8 @@ CASES = [
     ("stumps", dict(n_rounds=50, num_class=4, max_depth=1, num_feature=9, seed=16), 2_000),
     ("leaves_only", dict(n_rounds=5, num_class=4, max_depth=0, num_feature=9, seed=17), 500),
     ("deep_d10", dict(n_rounds=2, num_class=4, max_depth=10, num_feature=64, seed=18, p_stop=0.05), 1_500),
+    # depth 5 with an odd feature count: the LDS-staged walk's tree slots sit past an odd-sized tile
+    ("odd_features_d5", dict(n_rounds=12, num_class=4, max_depth=5, num_feature=259, seed=19), 2_000),
 ]
 
 

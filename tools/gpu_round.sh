@@ -74,6 +74,15 @@ xgb)  # kernel-trace stats + FETCH_SIZE pass of the XGB member (bench_configs --
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/fetch_xgb" -o run --output-format csv -- python3 "$ROOT/tools/bench_configs.py" --only 7 > "$OUT/prof_fetch_xgb.log" 2>&1
   step $? "fetch xgb"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs or xgb" >&2; exit 2 ;;
+mpmc)  # PMC passes over the member kernels (tools/members_pmc.py): SQ occupancy/stall/VALU/LDS, TA/TCP gather load
+  cd /tmp
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/mpmc_sq" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" > "$OUT/mpmc_sq.log" 2>&1
+  step $? "mpmc sq"
+  timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum -d "$OUT/prof/mpmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" > "$OUT/mpmc_ta.log" 2>&1
+  step $? "mpmc ta"
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS -d "$OUT/prof/mpmc_sq2" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" > "$OUT/mpmc_sq2.log" 2>&1
+  step $? "mpmc sq2"
+  ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb or mpmc" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
