@@ -384,6 +384,27 @@ def test_merge_lists_vs_oracle(ce, nl, q):
     assert np.array_equal(idx_np(i), io)
 
 
+@pytest.mark.parametrize("nl,q", [(1024, 10), (1000, 16), (700, 3)])
+def test_merge_survivor_overflow(ce, nl, q):
+    """The floor merge's overflow path: list i holds the values of ranks
+    q*i .. q*i+q-1, so the floor (the rank-(q-1) head of 64 group bests of 16
+    lists) admits ~16*q*q candidates -- more than its 1024 LDS slots for the
+    first two cases -- and the register lists + tree merge take over."""
+    from oracle import ce_oracle as O
+
+    n = nl * q
+    vals = np.linspace(2.0, 1.0, n).reshape(nl, q)
+    idx = np.arange(n, dtype=np.int64)[::-1].copy().reshape(nl, q)
+    v, i = ce.ops.topq_merge(dev(vals.ravel()), dev(idx.ravel()), q)
+    vo, io = O.oracle_topq_merge(vals.ravel(), idx.ravel(), q)
+    assert np.array_equal(idx_np(i), io) and np.array_equal(v.cpu().numpy(), vo)
+    # all equal: only the position order decides (lists best-first: ascending positions)
+    vals[:] = 0.5
+    idx = np.sort(idx, axis=1)
+    v, i = ce.ops.topq_merge(dev(vals.ravel()), dev(idx.ravel()), q)
+    assert np.array_equal(idx_np(i), O.oracle_topq_merge(vals.ravel(), idx.ravel(), q)[1])
+
+
 @pytest.mark.parametrize("N", [1, 63, 64, 65, 1608, 4096, 16384])
 def test_small_pool_single_launch(ce, N):
     """Pools under kSmallPoolBytes: one 16-wave block scores and selects."""
