@@ -822,3 +822,34 @@ def test_chunked_pool_vs_oracle(ce, C, dt, N, chunk):
     chunks = [(Pd[lo:lo + chunk], lo) for lo in range(0, N, chunk)][::-1]
     _, idx = ce.ops.select_mc_chunks(chunks, 10, "NMC")
     assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
+
+
+def test_c5_full_pool_chunk_invariance(ce):
+    """BASELINE configs[4] at its FULL size (50M items x 32 x 1000 bf16, 3.2 TB,
+    streamed as the bench streams it: device-generated 250K-item chunks): a
+    size-independent property the oracle cannot afford at 3.2 TB -- the
+    selection must not depend on where the chunk boundaries fall.  Job A adds
+    every chunk whole, job B the same bytes as two 125K-item halves (twice as
+    many boundaries, every running merge different); both must return the
+    same positions and bit-identical entropies, and the same positions as a
+    single-launch ce_select_mc over the chunk that holds the winner."""
+    items, nc, M, C, q = 50_000_000, 250_000, 32, 1000, 10
+    buf = torch.empty((nc, M, C), dtype=torch.bfloat16, device="cuda")
+    ja, jb = ce.ops.MCChunkJob(q, "NMC"), ce.ops.MCChunkJob(q, "NMC")
+    h = nc // 2
+    for c in range(items // nc):
+        lo = c * nc
+        buf.uniform_(0.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1987 * 100_003 + c))
+        ja.add(buf, lo)
+        jb.add(buf[:h], lo)
+        jb.add(buf[h:], lo + h)
+    va, ia = ja.result()
+    vb, ib = jb.result()
+    assert torch.equal(ia, ib) and torch.equal(va.view(torch.int64), vb.view(torch.int64))
+    assert ia.min().item() >= 0 and ia.max().item() < items
+    # the winner's own chunk, re-generated and selected in one launch, ranks it first
+    c0 = int(ia[0].item()) // nc
+    buf.uniform_(0.0, 1.0, generator=torch.Generator(device="cuda").manual_seed(1987 * 100_003 + c0))
+    v1, i1 = ce.ops.select_mc(buf, q, "NMC", base_idx=c0 * nc)
+    assert int(i1[0].item()) == int(ia[0].item())
+    assert v1[0].view(torch.int64).item() == va[0].view(torch.int64).item()
