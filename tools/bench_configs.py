@@ -207,7 +207,7 @@ def main():
     if 4 in only:  # configs[4]: 50M x 32 x 1000 bf16 (3.2 TB) streamed in chunks; here the first 5M items
         from tools.bench_c5 import run as c5_run
 
-        print(json.dumps(c5_run(items=5_000_000, log=False)), flush=True)  # full job: tools/bench_c5.py
+        print(json.dumps(c5_run(items=5_000_000, chunk=1_000_000, log=False)), flush=True)  # full job: tools/bench_c5.py
     if 5 in only:
         segment_mean_configs(g, report)
     if 6 in only:  # §8(f)4: member inference over 260-feature frames (GNB, SGD log), C = 4
