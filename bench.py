@@ -213,10 +213,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    # CE_AMD_REHEARSAL=1: several ranks share the visible GPUs over gloo (a
+    # one-GPU rehearsal of the multi-GPU code path; never used for a bench line)
+    rehearsal = os.environ.get("CE_AMD_REHEARSAL") == "1"
+    if rehearsal:
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     import ce_amd
     from ce_amd import dist as cdist

@@ -129,3 +129,30 @@ def test_rccl_sharded_mix_and_batched_world1():
             assert np.array_equal(i3[u].cpu().numpy(), eu)
     finally:
         dist.destroy_process_group()
+
+
+def test_bench_world2_rehearsal():
+    """bench.py's multi-GPU path end to end (shard generation, stage 1, stage 2
+    into ce_cand records, the all-gather, the merge, max-over-ranks timing, the
+    JSON line) with two ranks sharing the one GPU over gloo
+    (CE_AMD_REHEARSAL=1): it must select what the single-process run selects
+    on the same pool.  The real N-GPU run (RCCL, one rank per GPU) is the
+    driver's."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    args = ["bench.py", "--steps", "3", "--warmup", "1", "--n-items", "3000001", "--no-cpu-baseline"]
+    one = subprocess.run([sys.executable] + args, cwd=root, capture_output=True, text=True, timeout=600, env=env)
+    assert one.returncode == 0, one.stderr[-2000:]
+    env2 = dict(env, CE_AMD_REHEARSAL="1")
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args[:1] +
+                         ["--gpus", "2"] + args[1:], cwd=root, capture_output=True, text=True, timeout=600, env=env2)
+    assert two.returncode == 0, two.stderr[-2000:]
+    l1 = json.loads(one.stdout.strip().splitlines()[-1])
+    l2 = json.loads(two.stdout.strip().splitlines()[-1])
+    assert l2["n_gpus"] == 2 and l2["config"]["items_per_gpu"] == 1500001
+    assert l1["selected"] == l2["selected"] and len(l1["selected"]) == 10
