@@ -51,6 +51,10 @@ constexpr int kXgbPad = 65;       // LDS column stride (floats)
 constexpr int kXgbMaxDepth = 10;  // packed depth limit (2^10 leaves per tree)
 constexpr int kXgbMaxFeat = 512;
 constexpr int kXgbMaxGroups = 8;
+#ifndef CE_XGB_SCALAR_L1
+#define CE_XGB_SCALAR_L1 1
+#endif
+constexpr bool kXgbScalarL1 = CE_XGB_SCALAR_L1;
 
 // glibc expf (sysdeps/ieee754/flt-32/e_expf.c, EXP2F_TABLE_BITS = 5), as the
 // x86-64 FMA ifunc variant evaluates it: tab[i] = bits(2^(i/32)) - (i << 52) / 32.
@@ -215,7 +219,24 @@ struct WalkForest {
 #pragma unroll
             for (int j = 0; j < 8; ++j) idx[j] = go_right<MISS>(r[j], xs, D, lane) ? 2 : 1;
         }
-        for (int lev = 1; lev < depth; ++lev) {
+        int lev0 = 1;
+        if (depth >= 2 && kXgbScalarL1) {
+            // level 1 from the wave-uniform pair {node 1, node 2} (scalar loads) and a
+            // per-lane select: one gather instruction fewer per tree (the walk is
+            // bound by the texture path's address rate: TA 79 % busy; 4M frames
+            // 5.45 -> 4.88 ms).  Level 2 the same way (4 nodes, two selects) was
+            // slower (5.18 ms): the extra VALU outweighs the saved gather.
+            uint4 p1[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) p1[j] = *reinterpret_cast<const uint4*>(tn[j] + 1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint2 nd = idx[j] == 1 ? uint2{p1[j].x, p1[j].y} : uint2{p1[j].z, p1[j].w};
+                idx[j] = 2 * idx[j] + 1 + (go_right<MISS>(nd, xs, D, lane) ? 1 : 0);
+            }
+            lev0 = 2;
+        }
+        for (int lev = lev0; lev < depth; ++lev) {
             uint2 nd[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) nd[j] = tn[j][idx[j]];
