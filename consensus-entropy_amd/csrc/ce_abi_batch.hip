@@ -33,19 +33,7 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
         N_h <= 2 * kSmallBSWide && (C == 4 || C == 8)) {
         // both segments in ONE block (k_select_small, two segments)
         const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
-        bool launched = false;
-        rc = with_committee(a, [&](auto src) {
-            using S = decltype(src);
-            if constexpr (S::kC == 4 || S::kC == 8) {
-                constexpr int CC = S::kC;
-                if (vec_ok(t, CC))
-                    launch_small_mix(src, make_src<kF64, CC, true>(t), N, N_h, q, val_out, idx_out, st);
-                else
-                    launch_small_mix(src, make_src<kF64, CC, false>(t), N, N_h, q, val_out, idx_out, st);
-                launched = true;
-            }
-        });
-        if (rc == CE_OK && launched) return check_launch("ce_select_mix");
+        if (launch_small_mix(a, t, q, val_out, idx_out, st)) return check_launch("ce_select_mix");
     }
     // both segments on the streaming engine when it applies (q <= 64): the hc
     // table is a committee of M = 1 member ([N_h, 1, C] f64, row stride ld_hc)
@@ -61,12 +49,8 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
         return check_launch("ce_select_mix");
     }
     Seg s2{nullptr, N_h, G2, N};
-    switch (C) {
-#define CE_T(CC) case CC: launch_partial(TableSrc<CC>{hc, ld_hc}, s2, G2, q, w2, nullptr, nullptr, false, st); break;
-        CE_T(2) CE_T(3) CE_T(4) CE_T(8)
-#undef CE_T
-        default: return fail(CE_EUNSUPPORTED, "mix with C=%d has no kernel in this build", C);
-    }
+    if (partial_table(hc, ld_hc, C, s2, G2, q, w2, st) != CE_OK)
+        return fail(CE_EUNSUPPORTED, "mix with C=%d has no kernel in this build", C);
     finish_lists(w, 1, G1 + G2, q, val_out, idx_out, st);
     return check_launch("ce_select_mix");
 }
@@ -107,30 +91,13 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     if (small_enabled() && q <= kStreamMaxQ) {
         // one 512-thread block per user when the average user fits one sweep
         // (k_select_small; a longer user streams inside its block)
-        bool launched = false;
-        rc = with_committee(a, [&](auto src) {
-            using S = decltype(src);
-            if (cdiv(total_items, U) <= (int64_t)kSmallBS * small_ipt<S>()) {
-                launch_small<S, kSmallBS>(src, U, offsets, 0, 0, q, val_out, idx_out, nullptr, st);
-                launched = true;
-            }
-        });
-        if (rc == CE_OK && launched) return check_launch("ce_select_batched");
+        if (launch_small_users(a, offsets, U, q, val_out, idx_out, st)) return check_launch("ce_select_batched");
     }
     if (stream_enabled() && q <= kStreamMaxQ) {
         // bpu 4-wave blocks per user, then one wave per user merges its bpu lists
-        rc = with_committee(a, [&](auto src) {
-            using S = decltype(src);
-            with_seg_batching<S>([&](auto unr, auto ipl) {
-                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>),
-                                   dim3((unsigned)nl), dim3(bpu == 1 && U < 64 ? 64 * kSegWaves : 256), 0, st, src, offsets,
-                                   (int64_t)0, (int64_t)0, q, bpu, val_out, idx_out, w.c, (const uint32_t*)nullptr);
-            });
-        });
-        if (rc == CE_OK) {
-            if (bpu > 1)
-                hipLaunchKernelGGL((k_merge_wave<false>), dim3((U + 3) / 4), dim3(256), 0, st,
-                                   ListSrc<false>{w.c, nullptr, nullptr}, U, bpu, q, val_out, idx_out);
+        if (launch_seg(a, offsets, 0, 0, q, (int)nl, bpu, bpu == 1 && U < 64 ? 64 * kSegWaves : 256, val_out, idx_out,
+                       w.c, nullptr, st)) {
+            if (bpu > 1) launch_merge_wave(w.c, U, bpu, q, val_out, idx_out, st);
             return check_launch("ce_select_batched");
         }
     }

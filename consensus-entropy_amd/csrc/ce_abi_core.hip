@@ -265,7 +265,7 @@ extern "C" int ce_topq(const double* ent, int64_t N, int32_t q, int64_t base_idx
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, G, q);
     Seg sg{nullptr, N, G, base_idx};
-    launch_partial(ArraySrc{ent}, sg, G, q, w, val_out, idx_out, G == 1, st);
+    partial_entropies(ent, sg, G, q, w, val_out, idx_out, G == 1, st);
     if (G > 1) finish_lists(w, 1, G, q, val_out, idx_out, st);
     return check_launch("ce_topq");
 }
@@ -275,8 +275,7 @@ extern "C" int ce_topq_merge(const double* vals, const int64_t* idx, int32_t nli
     int rc = check_q(q);
     if (rc) return rc;
     if (nlists < 1 || !vals || !idx || !val_out || !idx_out) return fail(CE_EINVAL, "bad merge arguments");
-    ListSrc<true> ls{nullptr, vals, idx};
-    launch_finish(ls, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
+    launch_finish_vals(vals, idx, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
     return check_launch("ce_topq_merge");
 }
 

@@ -62,18 +62,7 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
     if (!ws || ws_bytes < lists_bytes(pool_blocks(N), q)) return fail(CE_EWORKSPACE, "workspace too small");
     if (small_enabled() && q <= kStreamMaxQ && N > 0) {
         // one block scores and selects the whole pool (k_select_small)
-        bool launched = false;
-        const int rc = with_committee(a, [&](auto src) {
-            using S = decltype(src);
-            if (N <= (int64_t)kSmallBS * small_ipt<S>()) {
-                launch_small<S, kSmallBS>(src, 1, nullptr, N, base_idx, q, val_out, idx_out, excl, st);
-                launched = true;
-            } else if (N <= (int64_t)kSmallBSWide * small_ipt<S>()) {
-                launch_small<S, kSmallBSWide>(src, 1, nullptr, N, base_idx, q, val_out, idx_out, excl, st);
-                launched = true;
-            }
-        });
-        if (rc == CE_OK && launched) return check_launch("ce_select_mc");
+        if (launch_small_pool(a, base_idx, q, val_out, idx_out, excl, st)) return check_launch("ce_select_mc");
     }
     if (stream_enabled() && q <= kStreamMaxQ && N > 0 &&
         N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes) {
@@ -81,17 +70,8 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
         // is the final answer), then one wave merges the blocks' lists
         const int nb = (int)std::min<int64_t>(std::min<int64_t>(cdiv(N, 512), 32), pool_blocks(N));
         WsLists w = carve(ws, nb, q);
-        const int rc = with_committee(a, [&](auto src) {
-            using S = decltype(src);
-            with_seg_batching<S>([&](auto unr, auto ipl) {
-                hipLaunchKernelGGL((k_stream_seg<S, decltype(ipl)::value, decltype(unr)::value, kSegWaves>), dim3(nb),
-                                   dim3(256), 0, st, src, nullptr, N, base_idx, q, nb, val_out, idx_out, w.c, excl);
-            });
-        });
-        if (rc == CE_OK) {
-            if (nb > 1)
-                hipLaunchKernelGGL((k_merge_wave<false>), dim3(1), dim3(256), 0, st, ListSrc<false>{w.c, nullptr, nullptr},
-                                   1, nb, q, val_out, idx_out);
+        if (launch_seg(a, nullptr, N, base_idx, q, nb, nb, 256, val_out, idx_out, w.c, excl, st)) {
+            if (nb > 1) launch_merge_wave(w.c, 1, nb, q, val_out, idx_out, st);
             return check_launch("ce_select_mc");
         }
     }
@@ -144,8 +124,7 @@ extern "C" int ce_select_finish_cands(int64_t N, int32_t q, void* ws, size_t ws_
     if ((uintptr_t)out % 16) return fail(CE_EINVAL, "ce_cand output must be 16-byte aligned");
     const int G = pool_blocks(N);
     if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
-    ListSrc<false> ls{carve(ws, G, q).c, nullptr, nullptr};
-    launch_finish(ls, 1, G, q, nullptr, nullptr, (hipStream_t)stream, reinterpret_cast<Cand*>(out));
+    launch_finish_lists(carve(ws, G, q).c, 1, G, q, nullptr, nullptr, (hipStream_t)stream, reinterpret_cast<Cand*>(out));
     return check_launch("ce_select_finish_cands");
 }
 
@@ -155,8 +134,7 @@ extern "C" int ce_merge_cands(const ce_cand* c, int32_t nlists, int32_t q, doubl
     if (rc) return rc;
     if (nlists < 1 || !c || !val_out || !idx_out) return fail(CE_EINVAL, "bad merge arguments");
     if ((uintptr_t)c % 16) return fail(CE_EINVAL, "ce_cand input must be 16-byte aligned");
-    ListSrc<false> ls{reinterpret_cast<const Cand*>(c), nullptr, nullptr};
-    launch_finish(ls, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
+    launch_finish_lists(reinterpret_cast<const Cand*>(c), 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
     return check_launch("ce_merge_cands");
 }
 
@@ -198,7 +176,7 @@ extern "C" int ce_select_mc_chunk(const void* p, ce_dtype dt, int64_t N, int32_t
     bool fin = false;
     rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &Gs, &fin, st);
     if (rc) return rc;
-    launch_finish(ListSrc<false>{w.c, nullptr, nullptr}, 1, G + (first ? 0 : 1), q, nullptr, nullptr, st, run);
+    launch_finish_lists(w.c, 1, G + (first ? 0 : 1), q, nullptr, nullptr, st, run);
     return check_launch("ce_select_mc_chunk");
 }
 

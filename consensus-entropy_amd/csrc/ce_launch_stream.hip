@@ -1,0 +1,83 @@
+// ce_launch_stream.hip -- the streaming stage-1 launcher (the only TU that
+// instantiates k_stream_nmc / k_stream_direct / k_stream_wide2 / k_stream_wide).
+#include "ce_host.hpp"
+
+using namespace ce;
+
+// (UNR members x IPL items) loads in flight per lane for the direct paths:
+// small committees batch items, large ones batch members.
+template <class Src, class F>
+static inline void with_batching(int M, F&& f) {
+    if constexpr (Src::kDT == kF64 || Src::kC > 4) {
+        (void)M;
+        f(std::integral_constant<int, 4>(), std::integral_constant<int, 2>());
+    } else {
+        if (M <= 4) f(std::integral_constant<int, 4>(), std::integral_constant<int, 4>());
+        else f(std::integral_constant<int, 8>(), std::integral_constant<int, 2>());
+    }
+}
+
+
+// Launches the streaming kernel when it applies; returns false otherwise.
+bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
+                   const uint32_t* excl) {
+    if (!stream_enabled() || q > kStreamMaxQ || a.N == 0) return false;
+    StreamArgs sa = stream_args(a, G, base_idx);
+    sa.excl = excl;
+    const int eb = elem_bytes(a.dt);
+    const int64_t R = (int64_t)a.M * a.C * eb;
+    const bool dense_nmc = a.sC == 1 && a.sM == a.C && a.sN == (int64_t)a.M * a.C && (uintptr_t)a.p % 16 == 0;
+    if (dense_nmc && (R == 256 || R == 512)) {
+#define CE_S(DT_, C_, S_)                                                                                   \
+    if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
+        auto kern = dma_nt() ? k_stream_nmc<DT_, C_, S_, 2> : k_stream_nmc<DT_, C_, S_, 0>;              \
+        const int grid = resident_grid(kern, 0, G);                                                       \
+        stream_grid(sa, grid);                                                                            \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                               \
+        return true;                                                                                      \
+    }
+        CE_S(kF32, 4, 16) CE_S(kF32, 4, 32) CE_S(kBF16, 4, 16) CE_S(kBF16, 4, 32) CE_S(kF64, 4, 32)
+        CE_S(kF32, 8, 16) CE_S(kF32, 8, 32)
+#undef CE_S
+    }
+    int rc = with_committee(a, [&](auto src) {
+        using S = decltype(src);
+        with_batching<S>(a.M, [&](auto unr, auto ipl) {
+            auto kern = k_stream_direct<S, decltype(ipl)::value, decltype(unr)::value>;
+            const int grid = resident_grid(kern, 0, G);
+            stream_grid(sa, grid);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, src, sa, q, w.c);
+        });
+    });
+    if (rc == CE_OK) return true;
+    const WideArgs wa = wide_args(a);
+    const PwPlan pl = pw_plan(a.C);
+    const size_t lds = wide_lds_bytes(a.C);
+    int rc_excl = CE_OK;
+    rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
+        constexpr int DT = decltype(dt)::value, NPL = decltype(npl)::value;
+        if constexpr (decltype(vec)::value) {
+            if (wide2_enabled()) {
+                constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
+                // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
+                constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
+                // a 2-batch register ring (3 and 4 measured: 72.8 / 71.9 % vs 72.6 % at C5)
+                auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
+                const int grid = resident_grid(kern, lds, G);
+                stream_grid(sa, grid);
+                sa.per_wave = cdiv(a.N, (int64_t)grid * 4);  // whole items, not 64-item tiles
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
+                return;
+            }
+        }
+        if (sa.excl) {  // k_stream_wide takes no bitmap
+            rc_excl = CE_EUNSUPPORTED;
+            return;
+        }
+        auto kern = k_stream_wide<DT, NPL, decltype(vec)::value>;
+        const int grid = resident_grid(kern, lds, G);
+        stream_grid(sa, grid);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
+    });
+    return rc == CE_OK && rc_excl == CE_OK;
+}
