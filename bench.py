@@ -9,16 +9,17 @@ the SAME pool is sharded over the ranks (strong scaling, as the north star's
 "6x at 8 GPUs on the 100M-item pool" asks) and the ranks exchange their local
 top-q with one RCCL all-gather before an identical merge on every rank.
 
-One step = the full selection: fused score + per-block top-q over the resident
-shard (stage 1, the streaming kernel), the merge of the blocks' candidates
-(stage 2), and for N > 1 the all-gather of every rank's q candidate records
-(16 B each) + the merge.  Inputs are synthetic
+One step = the full selection: ONE kernel per rank -- fused score + per-block
+top-q over the resident shard (the streaming stage 1) whose last block merges
+the blocks' candidates (stage 2 folded in) -- and for N > 1 the all-gather of
+every rank's q candidate records (16 B each) + the merge.  Inputs are synthetic
 Dirichlet(1) member rows (1% un-normalised, like sigmoid CNN members), seed
 1987, generated on the device before timing.
 
 Also reported:
-  roofline      stage-1 kernel: algorithmic bytes (N_local x 256 B) / its mean
-                duration from HIP events on the launch stream, vs 8 TB/s;
+  roofline      the selection kernel (stage 1 + folded stage 2): algorithmic
+                bytes (N_local x 256 B) / its mean duration from HIP events on
+                the launch stream, vs 8 TB/s;
                 traffic = HBM bytes per launch from the committed rocprofv3 PMC
                 pass (profiles/), or null
   cpu_baseline  the reference's own expressions (amg_test.py:441-445, numpy +
@@ -47,8 +48,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 # the stage-1 kernel each layout launches at M=16, C=4, f32, q <= 64 (ce_kernels.hip launch_stream)
 STAGE1_KERNEL = {
-    "NMC": "ce::k_stream_nmc<f32, C=4, S=16> (item-major, LDS-DMA tiles)",
-    "MNC": "ce::k_stream_direct<CommitteeSrc<f32, C=4, vec>, IPL=2, UNR=8> (member-major, direct loads)",
+    "NMC": "ce::k_stream_nmc<f32, C=4, S=16> (item-major, LDS-DMA tiles; stage 2 folded into the last block)",
+    "MNC": "ce::k_stream_direct<CommitteeSrc<f32, C=4, vec>, IPL=2, UNR=8> (member-major, direct loads; stage 2 folded)",
 }
 
 
@@ -220,15 +221,12 @@ def main():
         local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=device)
-
     import ce_amd
     from ce_amd import dist as cdist
     from ce_amd import ops
+
+    if world > 1:  # fail fast: a dead rank ends the job within the timeout (ce_amd.dist.init)
+        cdist.init("gloo" if rehearsal else "nccl", device=device)
 
     ce_amd.load()
     N, M, C, q = args.n_items, args.members, args.classes, args.q
@@ -248,22 +246,26 @@ def main():
     send = torch.empty((q, 2), dtype=torch.int64, device=device)
     recv = torch.empty((world * q, 2), dtype=torch.int64, device=device)
 
-    def finish():
+    def local():
+        """This rank's selection kernel: ONE launch (stage 2 folded into the
+        streaming stage 1's last block) -> final (vals, idx) at N = 1, the
+        rank's q candidate records (the all-gather send buffer) at N > 1."""
         if world == 1:
-            return plan.finish()
+            return plan.step()
         if q > 64:  # records need q <= 64: exchange packed (entropy, position) pairs instead
-            vals, idx = plan.finish()
-            return ops.topq_merge(*cdist.allgather_topq(vals, idx, q), q)
-        plan.finish_cands(send)
+            return plan.step()
+        return plan.step_cands(send)
+
+    def exchange(loc):
+        if world == 1:
+            return loc
+        if q > 64:
+            return ops.topq_merge(*cdist.allgather_topq(*loc, q), q)
         cdist.allgather_cands(send, out=recv)
         return ops.merge_cands(recv, q)
 
-    def step():
-        plan.partial()
-        return finish()
-
     for _ in range(args.warmup):
-        step()
+        exchange(local())
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
@@ -272,9 +274,9 @@ def main():
     t_start = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        plan.partial()
+        loc = local()
         ev[k][1].record(stream)
-        vals, idx = finish()
+        vals, idx = exchange(loc)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -330,6 +332,10 @@ def main():
             "cpu_baseline": None,
             "selected": picks,
         }
+        if rehearsal:  # ranks sharing one GPU over gloo: a code-path rehearsal, not a multi-GPU figure
+            line["rehearsal"] = {"backend": "gloo", "gpus_visible": torch.cuda.device_count(),
+                                 "note": "NOT a multi-GPU measurement"}
+            line["value"] = None
         if world == 1 and not args.no_cpu_baseline:
             del P, plan
             torch.cuda.empty_cache()

@@ -52,6 +52,7 @@ SIGNATURES = {
     "ce_select_finish": (_int, [_i64, _i32, _vp, _sz, _vp, _vp, _vp]),
     "ce_select_finish_cands": (_int, [_i64, _i32, _vp, _sz, _vp, _vp]),
     "ce_merge_cands": (_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
+    "ce_select_mc_cands": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _i32, _i64, _vp, _sz, _vp, _vp]),
     "ce_select_mc_chunk_workspace_bytes": (_sz, [_i64, _i32]),
     "ce_select_mc_chunk": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _i32, _i64, _vp, _i32, _vp, _sz,
                                   _vp]),

@@ -16,6 +16,12 @@ The local-select and merge steps are injectable so the collective logic can be
 exercised on CPU with the gloo backend (tests/test_dist.py); by default they
 are the HIP operators.
 
+Validation status: every sharded path is tested against the CPU restatement on the gloo
+backend at world 2 and 3 (tests/test_dist.py) and through the HIP kernels with
+RCCL at world 1 (tests/test_gpu_dist.py); RCCL with more than one rank runs
+only in the driver's multi-GPU bench (bench.py), so multi-rank exactness is
+validated on gloo.
+
 The other sharded configs of SURVEY.md §8(e): the mix stack [mc; hc] sharded
 over its concatenated index space (sharded_select_mix), batched users sharded
 over ranks with only a final gather (sharded_select_batched), and pools larger
@@ -23,10 +29,34 @@ than HBM streamed per rank (sharded_select_mc_chunks).
 """
 from __future__ import annotations
 
+import datetime
+import os
+
 import torch
 import torch.distributed as dist
 
 from . import ops
+
+DEFAULT_TIMEOUT_S = 120.0
+
+
+def init(backend="nccl", *, device=None, timeout_s=None):
+    """Join the process group (one process per GPU; RANK / WORLD_SIZE /
+    MASTER_* from the environment, as torchrun sets them) with FAIL-FAST
+    error handling: every collective, the rendezvous included,
+    gives up after ``timeout_s`` (default CE_AMD_DIST_TIMEOUT_S or 120 s;
+    torch's own default is 10 minutes), and on the RCCL backend a failed or
+    timed-out collective tears the process down (TORCH_NCCL_ASYNC_ERROR_HANDLING
+    = 1) instead of leaving the survivors blocked on a dead rank.  The selection
+    exchanges 16q bytes per rank per step (microseconds), so any wait of that
+    order means a lost rank."""
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("CE_AMD_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = {"timeout": datetime.timedelta(seconds=float(timeout_s))}
+    if device is not None and backend == "nccl":
+        kw["device_id"] = torch.device(device)
+    dist.init_process_group(backend, **kw)
 
 
 def shard_range(n, rank, world):
@@ -75,15 +105,13 @@ def sharded_select_mc_records(P_local, q, *, global_offset, layout="NMC", group=
     the merge reads the receive buffer.
 
     local_records  f(P_local, q, base_idx) -> int64 [q, 2] records; default
-                   the HIP stages (ops.MCPlan + finish_cands)
+                   the HIP selection in one launch (ops.MCPlan.step_cands)
     merge_records  f(records [world*q, 2], q) -> (vals, idx); default
                    ops.merge_cands (HIP)
     """
     if local_records is None:
         def local_records(P, qq, base):
-            plan = ops.MCPlan(P, qq, layout, base_idx=base)
-            plan.partial()
-            return plan.finish_cands()
+            return ops.MCPlan(P, qq, layout, base_idx=base).step_cands()
     if merge_records is None:
         merge_records = ops.merge_cands
     rec = local_records(P_local, q, int(global_offset))

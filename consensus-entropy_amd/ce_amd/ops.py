@@ -32,6 +32,13 @@ def _on_gpu(t, what):
         raise ValueError(f"{what} must live on a HIP device (got {t.device}); there is no CPU path")
 
 
+def new_workspace(nbytes, device):
+    """A workspace for the engine: zero-filled, as include/ce.h requires (its
+    header holds the tiled kernels' arrival counters, which every call leaves
+    zero again)."""
+    return torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
 class _WorkspaceCache:
     """Per-device scratch reused across calls (grows, never shrinks), so steady
     state allocates nothing."""
@@ -43,7 +50,7 @@ class _WorkspaceCache:
         key = torch.device(device).index
         buf = self._ws.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            buf = new_workspace(nbytes, device)
             self._ws[key] = buf
         return buf
 
@@ -311,9 +318,10 @@ def mark_selected(excl, n, idx, base_idx=0):
 
 
 class MCPlan:
-    """Pre-bound two-stage mc selection (stage 1 = the streaming kernel, stage 2
-    = the merge), with its own workspace and outputs: what the bench and the
-    multi-GPU driver launch every step."""
+    """Pre-bound mc selection with its own workspace and outputs: what the
+    bench and the multi-GPU driver launch every step.  step() / step_cands()
+    run the whole selection in one launch; partial() + finish() /
+    finish_cands() are the two stages as separate launches."""
 
     def __init__(self, P, q, layout="NMC", base_idx=0):
         self.P = P
@@ -322,7 +330,7 @@ class MCPlan:
         self.base_idx = int(base_idx)
         lib = _lib.load()
         self.ws_bytes = lib.ce_select_mc_workspace_bytes(self.N, self.q)
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=P.device)
+        self.ws = new_workspace(self.ws_bytes, P.device)
         self.vals, self.idx = _outs(self.q, P.device)
 
     def partial(self):
@@ -343,9 +351,24 @@ class MCPlan:
         call("ce_select_finish_cands", self.N, self.q, _p(self.ws), self.ws_bytes, _p(out), _stream(self.P.device))
         return out
 
+    def step(self):
+        """The whole selection in ONE launch (ce_select_mc: stage 2 folded into
+        stage 1's last block for q <= 64): (vals [q], idx [q])."""
+        call("ce_select_mc", _p(self.P), self.dt, self.N, self.M, self.C, self.sN, self.sM, self.sC, self.q,
+             self.base_idx, _p(self.ws), self.ws_bytes, _p(self.vals), _p(self.idx), _stream(self.P.device))
+        return self.vals, self.idx
+
+    def step_cands(self, out=None):
+        """This pool's q candidate records (int64 [q, 2], the multi-GPU send
+        buffer) in ONE launch (ce_select_mc_cands).  q <= 64."""
+        if out is None:
+            out = torch.empty((self.q, 2), dtype=torch.int64, device=self.P.device)
+        call("ce_select_mc_cands", _p(self.P), self.dt, self.N, self.M, self.C, self.sN, self.sM, self.sC, self.q,
+             self.base_idx, _p(self.ws), self.ws_bytes, _p(out), _stream(self.P.device))
+        return out
+
     def __call__(self):
-        self.partial()
-        return self.finish()
+        return self.step()
 
 
 def merge_cands(cands, q):
@@ -383,14 +406,26 @@ class MCChunkJob:
         self.running = None
         self.n_items = 0
         self._fresh = True
+        self._ranges = []  # [lo, hi) position ranges added so far
 
     def add(self, P, base_idx=None):
         """Score chunk P (layout as constructed); its items are pool positions
         base_idx .. base_idx + N - 1 (default: right after the previous chunk)."""
         N, M, C, sN, sM, sC, dt = committee_view(P, self.layout)
         if self.running is None:
+            if self.device is not None and self.device.index is not None and P.device != self.device:
+                raise ValueError(f"chunk on {P.device}, job on {self.device}")
             self.running = torch.empty((self.q, 2), dtype=torch.int64, device=P.device)
+        elif P.device != self.running.device:
+            raise ValueError(f"chunk on {P.device}, but the job's running list lives on {self.running.device}")
         base = self.n_items if base_idx is None else int(base_idx)
+        if base < 0:
+            raise ValueError(f"base_idx must be >= 0, got {base}")
+        for lo, hi in self._ranges:  # a position scored twice would be merged silently
+            if base < hi and lo < base + N:
+                raise ValueError(f"chunk positions [{base}, {base + N}) overlap an added chunk [{lo}, {hi})")
+        if N > 0:
+            self._ranges.append((base, base + N))
         lib = _lib.load()
         ws = WORKSPACE.get(P.device, lib.ce_select_mc_chunk_workspace_bytes(N, self.q))
         first = 1 if self._fresh else 0

@@ -25,8 +25,16 @@ Modes (amg_test.py:425-489):
         part removes the song from both, as :484 + :521-531 do by id.
         Positions: i in [0, N) = committee item i, N + j = hc row j (the row
         stack [mc; hc] of select_queries, over the full pools)
-  rand  uniform among the remaining items with the caller's RandomState
-        (legacy np.random.shuffle of the remaining positions, first q)
+  rand  amg_test.py:486-489: ``pos_songs = X_train.index.unique().tolist();
+        np.random.shuffle(pos_songs); pos_songs[:q]`` -- the legacy shuffle of
+        the REMAINING songs in the order they first appear in X_train.
+        ``rand_order`` gives that order as positions (the pool position of the
+        first song of X_train, of the second, ...); the remaining songs keep it
+        as the pool shrinks (a DataFrame drop keeps row order), so with the
+        caller's RandomState (or the global one the reference seeds with
+        np.random.seed(1987), :55) the picks are the reference's, draw for
+        draw.  Default: ascending positions, i.e. X_train's songs appear in
+        position order.
 """
 from __future__ import annotations
 
@@ -39,7 +47,7 @@ from .select import MODES, _device, _hc_tensor, stack_committee
 
 class SelectionSession:
     def __init__(self, queries, mode, n_items, *, hc=None, votes=None, hc_to_mc=None, rng=None, device=None,
-                 n_classes=4):
+                 n_classes=4, rand_order=None):
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}, got {mode!r}")
         self.q = int(queries)
@@ -56,6 +64,12 @@ class SelectionSession:
                 self.N = self.H.shape[0]
         self.excl = ops.excl_bitmap(self.N, self.dev)
         self.n_selected = 0
+        self.rand_order = None
+        if mode == "rand":
+            order = np.arange(self.N) if rand_order is None else np.asarray(rand_order, dtype=np.int64).reshape(-1)
+            if order.shape[0] != self.N or not np.array_equal(np.sort(order), np.arange(self.N)):
+                raise ValueError("rand_order must be a permutation of the n_items pool positions")
+            self.rand_order = order
         if mode == "mix":
             Nh = self.H.shape[0]
             if hc_to_mc is None:
@@ -93,9 +107,9 @@ class SelectionSession:
         """One epoch: returns the q picked positions (np.int64; fewer when the
         pool runs dry) and removes them from the pool."""
         q = self.q
-        if self.mode == "rand":
+        if self.mode == "rand":  # amg_test.py:487-489 over the remaining songs, in X_train order
             keep = ~self._mask()
-            pool = np.flatnonzero(keep).tolist()
+            pool = self.rand_order[keep[self.rand_order]].tolist()
             (self.rng if self.rng is not None else np.random).shuffle(pool)
             pick = np.asarray(pool[:q], np.int64)
             ops.mark_selected(self.excl, self.N, torch.from_numpy(pick).to(self.dev))

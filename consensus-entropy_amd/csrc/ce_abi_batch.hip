@@ -4,11 +4,6 @@
 
 using namespace ce;
 
-#ifdef CE_PHASE_TIMING
-extern "C" int ce_debug_phase(uint64_t* host, int n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), (size_t)n * 6 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 // ---- fused mix ---------------------------------------------------------------
 extern "C" size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t q) {
@@ -29,11 +24,11 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     if (!ws || ws_bytes < lists_bytes((int64_t)G1 + G2, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, (int64_t)G1 + G2, q);
-    if (small_enabled() && q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= 2 * kSmallBSWide &&
-        N_h <= 2 * kSmallBSWide && (C == 4 || C == 8)) {
-        // both segments in ONE block (k_select_small, two segments)
+    if (small_enabled() && q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= kSmallPoolItems && N_h <= kSmallPoolItems &&
+        (C == 4 || C == 8)) {
+        // both segments in ONE launch: tiles of either segment, ticketed merge (k_select_tiles)
         const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
-        if (launch_small_mix(a, t, q, val_out, idx_out, st)) return check_launch("ce_select_mix");
+        if (launch_small_mix(a, t, q, val_out, idx_out, w, st)) return check_launch("ce_select_mix");
     }
     // both segments on the streaming engine when it applies (q <= 64): the hc
     // table is a committee of M = 1 member ([N_h, 1, C] f64, row stride ld_hc)
@@ -42,7 +37,7 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
         rc = committee_partial(a, s1, G1, q, w, nullptr, nullptr, false, st);
         if (rc) return dispatch_err(rc, a);
     }
-    WsLists w2{w.c + (size_t)G1 * q};
+    WsLists w2{w.c + (size_t)G1 * q, w.ctr};
     const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
     if (launch_stream(t, G2, q, N, w2, st)) {
         finish_lists(w, 1, G1 + G2, q, val_out, idx_out, st);
@@ -69,9 +64,15 @@ static int batched_bpu(int64_t total, int U) {
     return (int)bpu;
 }
 
+// lists of either batched path: bpu per user (k_stream_seg) or the tiles (k_select_tiles)
+static int64_t batched_lists(int64_t total_items, int U, int q) {
+    return (int64_t)std::max(batched_bpu(total_items, U), small_users_tiles(total_items, U, q)) * U;
+}
+
 extern "C" size_t ce_select_batched_workspace_bytes(int64_t total_items, int32_t U, int32_t q) {
     if (U < 1) U = 1;
-    return lists_bytes((int64_t)batched_bpu(total_items, U) * U, q < 1 ? 1 : q);
+    if (q < 1) q = 1;
+    return lists_bytes(batched_lists(total_items, U, q), q);
 }
 
 extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items, int32_t M, int32_t C, int64_t sN,
@@ -85,13 +86,14 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     if (U < 1 || !offsets || !val_out || !idx_out) return fail(CE_EINVAL, "bad batched arguments");
     const int bpu = batched_bpu(total_items, U);
     const int64_t nl = (int64_t)bpu * U;
-    if (!ws || ws_bytes < lists_bytes(nl, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (!ws || ws_bytes < lists_bytes(batched_lists(total_items, U, q), q))
+        return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, nl, q);
     if (small_enabled() && q <= kStreamMaxQ) {
-        // one 512-thread block per user when the average user fits one sweep
-        // (k_select_small; a longer user streams inside its block)
-        if (launch_small_users(a, offsets, U, q, val_out, idx_out, st)) return check_launch("ce_select_batched");
+        // each user over a few tiles, ticketed per-user merge (k_select_tiles; a
+        // user longer than its tiles streams inside them)
+        if (launch_small_users(a, offsets, U, q, val_out, idx_out, w, st)) return check_launch("ce_select_batched");
     }
     if (stream_enabled() && q <= kStreamMaxQ) {
         // bpu 4-wave blocks per user, then one wave per user merges its bpu lists

@@ -61,8 +61,9 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
     // the workspace contract holds on every path, even the one that does not touch it
     if (!ws || ws_bytes < lists_bytes(pool_blocks(N), q)) return fail(CE_EWORKSPACE, "workspace too small");
     if (small_enabled() && q <= kStreamMaxQ && N > 0) {
-        // one block scores and selects the whole pool (k_select_small)
-        if (launch_small_pool(a, base_idx, q, val_out, idx_out, excl, st)) return check_launch("ce_select_mc");
+        // the pool over a few tiles, ticketed merge, one launch (k_select_tiles)
+        if (launch_small_pool(a, base_idx, q, val_out, idx_out, excl, carve(ws, 0, q), st))
+            return check_launch("ce_select_mc");
     }
     if (stream_enabled() && q <= kStreamMaxQ && N > 0 &&
         N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes) {
@@ -75,19 +76,49 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
             return check_launch("ce_select_mc");
         }
     }
-    int G = 0;
-    bool fin = false;
-    int rc;
-    if (excl) {  // the streaming engine only (the q > 64 paths take no bitmap)
-        G = pool_blocks(N);
-        if (!stream_enabled() || !wide2_enabled() || !launch_stream(a, G, q, base_idx, carve(ws, G, q), st, excl))
-            return fail(CE_EUNSUPPORTED, "exclusion bitmap: no streaming kernel for this shape");
-    } else {
-        rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &G, &fin, st);
-        if (rc) return rc;
+    // large pools: the streaming stage 1 with stage 2 folded into its last block
+    const int G = pool_blocks(N);
+    const int sr = launch_stream_fold(a, G, q, base_idx, carve(ws, G, q), st, excl, FoldOut{val_out, idx_out, nullptr});
+    if (sr == 2) return check_launch("ce_select_mc");
+    if (sr == 1) {
+        finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
+        return check_launch("ce_select_mc");
     }
-    if (!fin) finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
+    if (excl) return fail(CE_EUNSUPPORTED, "exclusion bitmap: no streaming kernel for this shape");
+    int Gp = 0;
+    bool fin = false;
+    const int rc = mc_partial(a, q, base_idx, ws, ws_bytes, val_out, idx_out, true, &Gp, &fin, st);
+    if (rc) return rc;
+    if (!fin) finish_lists(carve(ws, Gp, q), 1, Gp, q, val_out, idx_out, st);
     return check_launch("ce_select_mc");
+}
+
+// ce_select_mc writing the pool's q candidate records (the multi-GPU send
+// buffer) in ONE launch: stage 1 with stage 2 folded into its last block.
+extern "C" int ce_select_mc_cands(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
+                                  int64_t sC, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes, ce_cand* out,
+                                  ce_stream_t stream) {
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    int rc = check_comm(a);
+    if (rc) return rc;
+    rc = check_q(q);
+    if (rc) return rc;
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "candidate records need q <= %d (got %d)", kStreamMaxQ, q);
+    if (!out || (uintptr_t)out % 16) return fail(CE_EINVAL, "ce_cand output must be 16-byte aligned device memory");
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, G, q);
+    Cand* oc = reinterpret_cast<Cand*>(out);
+    const int sr = N > 0 ? launch_stream_fold(a, G, q, base_idx, w, st, nullptr, FoldOut{nullptr, nullptr, oc}) : 0;
+    if (sr == 2) return check_launch("ce_select_mc_cands");
+    if (sr == 0) {  // no streaming kernel (or an empty pool): the block-synchronous stage 1
+        Seg sg{nullptr, N, G, base_idx};
+        rc = committee_partial(a, sg, G, q, w, nullptr, nullptr, false, st);
+        if (rc) return dispatch_err(rc, a);
+    }
+    launch_finish_lists(w.c, 1, G, q, nullptr, nullptr, st, oc);
+    return check_launch("ce_select_mc_cands");
 }
 
 extern "C" int ce_select_mc_partial(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,

@@ -14,6 +14,8 @@
 
 #include "ce_glibc_log.hpp"
 
+#include "ce_debug.hpp"
+
 namespace ce {
 
 enum DType : int { kF32 = 0, kF64 = 1, kBF16 = 2 };

@@ -30,15 +30,29 @@ static inline int pool_blocks(int64_t n) {
     return (int)g;
 }
 
-static inline size_t lists_bytes(int64_t nlists, int q) { return (size_t)nlists * (size_t)q * 16u + 256u; }
+// Workspace layout (every *_workspace_bytes / carve agree): a fixed header of
+// kWsCounters u32 arrival counters (the tiled kernels' tickets, one per
+// problem; zero at rest: the caller zero-fills the workspace once, every call
+// leaves the counters zero) followed by the candidate lists, 16 B per slot.
+// The header is the same for every entry point, so one workspace can serve
+// any sequence of calls.
+constexpr int kWsCounters = 16384;
+constexpr size_t kWsHeader = (size_t)kWsCounters * sizeof(uint32_t);  // 64 KiB
+static inline size_t lists_bytes(int64_t nlists, int q) {
+    return kWsHeader + (size_t)nlists * (size_t)q * 16u + 256u;
+}
 
 struct WsLists {
-    Cand* c;
+    Cand* c;        // candidate lists
+    uint32_t* ctr;  // arrival counters (header)
 };
 static inline WsLists carve(void* ws, int64_t nlists, int q) {
+    (void)nlists;
+    (void)q;
     uintptr_t p = ((uintptr_t)ws + 255) & ~(uintptr_t)255;
     WsLists w;
-    w.c = reinterpret_cast<Cand*>(p);
+    w.ctr = reinterpret_cast<uint32_t*>(p);
+    w.c = reinterpret_cast<Cand*>(p + kWsHeader);
     return w;
 }
 
@@ -223,6 +237,10 @@ static inline StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx)
     s.nlists = G;
     s.per_wave = 0;
     s.excl = nullptr;
+    s.ctr = nullptr;
+    s.oval = nullptr;
+    s.oidx = nullptr;
+    s.ocand = nullptr;
     return s;
 }
 
@@ -248,6 +266,17 @@ static inline int dispatch_err(int rc, const CommArgs& a) {
 // (wide classes).  Returns false (nothing launched) when no kernel applies.
 CE_HIDDEN bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                              const uint32_t* excl = nullptr);
+// The same with stage 2 folded in: the grid's last block merges the block
+// lists into the final (oval, oidx), or into q records at ocand (one launch
+// for the whole selection).  Returns 0 (no streaming kernel applies), 1
+// (launched WITHOUT the fold: the lists are in w, run a finish) or 2 (folded).
+struct FoldOut {
+    double* oval;
+    int64_t* oidx;
+    Cand* ocand;
+};
+CE_HIDDEN int launch_stream_fold(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
+                                 const uint32_t* excl, FoldOut out);
 // ce_launch_partial.hip: block-synchronous stage 1 (any q): committee,
 // precomputed entropies, an hc table.
 CE_HIDDEN int committee_partial(const CommArgs& a, const Seg& sg, int grid, int q, WsLists w, double* oval,
@@ -263,18 +292,20 @@ CE_HIDDEN void launch_finish_vals(const double* vals, const int64_t* idx, int se
                                   double* oval, int64_t* oidx, hipStream_t st);
 CE_HIDDEN void launch_merge_wave(const Cand* c, int segs, int nl, int q, double* oval, int64_t* oidx,
                                  hipStream_t st);
-// ce_launch_small.hip: pools small enough for single-block selection.
-constexpr int kSmallBS = 512;       // batched users: 2 blocks per CU, all 500 users resident
-constexpr int kSmallBSWide = 1024;  // one pool of up to 4096 items
-// one pool of a.N items (<= 4096, or <= 2048 for C = 8) in one block; false: too large / no kernel
+// ce_launch_small.hip: pools of a few thousand items, tiled over blocks with
+// an arrival-ticket merge (k_select_tiles, ce_small.hpp).
+constexpr int kTileBS = 256;
+// one pool of a.N items (<= kSmallPoolItems); false: too large / no kernel
+constexpr int64_t kSmallPoolItems = 4096;
 CE_HIDDEN bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval, int64_t* oidx,
-                                 const uint32_t* excl, hipStream_t st);
-// U users (offsets[U+1]) in one block each, when the average user fits one sweep
+                                 const uint32_t* excl, WsLists w, hipStream_t st);
+// U users (offsets[U+1]) in one launch, small_users_tiles() tiles per user
+CE_HIDDEN int small_users_tiles(int64_t total_items, int U, int q);
 CE_HIDDEN bool launch_small_users(const CommArgs& a, const int64_t* offsets, int U, int q, double* oval,
-                                  int64_t* oidx, hipStream_t st);
-// the mix of amg_test.py:473-480 ([mc; hc] rows, C = 4 or 8) in one block
+                                  int64_t* oidx, WsLists w, hipStream_t st);
+// the mix of amg_test.py:473-480 ([mc; hc] rows, C = 4 or 8) in one launch
 CE_HIDDEN bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, double* oval, int64_t* oidx,
-                                hipStream_t st);
+                                WsLists w, hipStream_t st);
 // k_stream_seg over `nblocks` blocks of `threads` (bpu blocks per segment)
 CE_HIDDEN bool launch_seg(const CommArgs& a, const int64_t* offsets, int64_t n, int64_t base_idx, int q, int nblocks,
                           int bpu, int threads, double* oval, int64_t* oidx, Cand* wc, const uint32_t* excl,

@@ -27,6 +27,7 @@
 #include "ce_topq.hpp"
 #include "ce_wide.hpp"
 #include "ce_stream.hpp"
+#include "ce_small.hpp"
 #include "ce_members.hpp"
 #include "ce_abi.hpp"
 
@@ -193,6 +194,7 @@ __global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, Cand* _
     __shared__ TopQSmem<CAP> sm;
     TopQ<CAP, kBS> tq(sm);
     tq.init();
+    CE_DASSERT(q >= 1 && q <= CAP);
     int64_t s0, lo, hi;
     seg_range(sg, s0, lo, hi);
     const int64_t rel = sg.base_idx - s0;
@@ -304,6 +306,7 @@ template <int DT, int KCH, int UNR, int NB = 2>
 __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    CE_DASSERT((int)gridDim.x <= sa.nlists && q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
     __shared__ WaveLists sm;
     extern __shared__ __attribute__((aligned(16))) double wsm[];
     constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
@@ -373,6 +376,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
         }
     }
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
+    if (sa.ctr) fold_merge<4>(sa, q, wc, sm);
 }
 
 template <int DT, int NPL, bool VEC>
@@ -395,23 +399,6 @@ __global__ __launch_bounds__(kBS) void k_wide_entropy_v(WideArgs a, PwPlan pl, d
 // candidates >= T can be selected -- the filter is exact and usually leaves
 // ~q survivors.
 // ---------------------------------------------------------------------------
-template <bool FROM_VALS>
-struct ListSrc {
-    const Cand* c;
-    const double* val;
-    const int64_t* idx;
-    __device__ __forceinline__ void get(int64_t j, uint64_t& k, int64_t& i) const {
-        if constexpr (FROM_VALS) {
-            i = idx[j];
-            k = order_key(val[j]);
-        } else {
-            const Cand x = c[j];
-            k = x.key;
-            i = x.idx;
-        }
-    }
-};
-
 __device__ __forceinline__ void wave_best(uint64_t& k, int64_t& i) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -601,6 +588,7 @@ __global__ __launch_bounds__(1024) void k_merge_reg(ListSrc<FROM_VALS> src, int 
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
     const int64_t L = (int64_t)nl * q;
+    CE_DASSERT(nl >= 1 && q >= 1 && q <= kStreamMaxQ);
     // the first round of candidate loads goes out before the head phase
     uint64_t k[PF];
     int64_t id[PF];
@@ -760,6 +748,7 @@ __global__ __launch_bounds__(kBS) void k_segment_mean(const void* __restrict__ f
         const int64_t n = t / C;
         const int c = (int)(t - n * C);
         const int64_t f0 = offsets[n], f1 = offsets[n + 1];
+        CE_DASSERT(f0 >= 0 && f0 <= f1);
         double sum = 0.0;
         int64_t cnt = 0;
         // batches of 8 frames: the 8 loads are issued together (clamped rows,

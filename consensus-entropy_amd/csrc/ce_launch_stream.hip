@@ -18,12 +18,49 @@ static inline void with_batching(int M, F&& f) {
 }
 
 
-// Launches the streaming kernel when it applies; returns false otherwise.
+// A/B knob: CE_AMD_MNC_DMA=0 -> member-major pools on the direct-load kernel
+static bool mnc_dma_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_MNC_DMA");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// A/B knob: CE_AMD_FOLD=0 -> stage 2 as its own launch even where it can be folded
+static bool fold_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_FOLD");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
+                              const uint32_t* excl, const FoldOut* fold);
+
 bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                    const uint32_t* excl) {
-    if (!stream_enabled() || q > kStreamMaxQ || a.N == 0) return false;
+    return launch_stream_impl(a, G, q, base_idx, w, st, excl, nullptr) != 0;
+}
+
+int launch_stream_fold(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
+                       const uint32_t* excl, FoldOut out) {
+    return launch_stream_impl(a, G, q, base_idx, w, st, excl, fold_enabled() ? &out : nullptr);
+}
+
+static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
+                              const uint32_t* excl, const FoldOut* fold) {
+    if (!stream_enabled() || q > kStreamMaxQ || a.N == 0) return 0;
     StreamArgs sa = stream_args(a, G, base_idx);
     sa.excl = excl;
+    if (fold) {  // kernels that fold read these; k_stream_wide (below) does not
+        sa.ctr = w.ctr;
+        sa.oval = fold->oval;
+        sa.oidx = fold->oidx;
+        sa.ocand = fold->ocand;
+    }
+    const int folded = fold ? 2 : 1;
     const int eb = elem_bytes(a.dt);
     const int64_t R = (int64_t)a.M * a.C * eb;
     const bool dense_nmc = a.sC == 1 && a.sM == a.C && a.sN == (int64_t)a.M * a.C && (uintptr_t)a.p % 16 == 0;
@@ -34,11 +71,28 @@ bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w,
         const int grid = resident_grid(kern, 0, G);                                                       \
         stream_grid(sa, grid);                                                                            \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                               \
-        return true;                                                                                      \
+        return folded;                                                                                    \
     }
         CE_S(kF32, 4, 16) CE_S(kF32, 4, 32) CE_S(kBF16, 4, 16) CE_S(kBF16, 4, 32) CE_S(kF64, 4, 32)
         CE_S(kF32, 8, 16) CE_S(kF32, 8, 32)
 #undef CE_S
+    }
+    // member-major stack (the reference's np.array(pred_prob) order) with
+    // 16-B member rows: LDS-DMA tiles of one 1 KiB run per member
+    const bool dense_mnc = a.sC == 1 && a.sN == a.C && a.C * eb == 16 && (a.sM * eb) % 16 == 0 &&
+                           (uintptr_t)a.p % 16 == 0 && a.M >= 4 && mnc_dma_enabled();
+    if (dense_mnc) {
+#define CE_SM(DT_, C_, M_)                                                                              \
+    if (a.dt == DT_ && a.C == C_ && a.M == M_) {                                                       \
+        auto kern = dma_nt() ? k_stream_nmc<DT_, C_, M_, 2, true> : k_stream_nmc<DT_, C_, M_, 0, true>; \
+        const int grid = resident_grid(kern, 0, G);                                                    \
+        stream_grid(sa, grid);                                                                         \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                            \
+        return folded;                                                                                 \
+    }
+        CE_SM(kF32, 4, 4) CE_SM(kF32, 4, 8) CE_SM(kF32, 4, 16) CE_SM(kF32, 4, 20) CE_SM(kF32, 4, 32)
+        CE_SM(kF64, 2, 8) CE_SM(kF64, 2, 16) CE_SM(kBF16, 8, 16)
+#undef CE_SM
     }
     int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
@@ -49,11 +103,12 @@ bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w,
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, src, sa, q, w.c);
         });
     });
-    if (rc == CE_OK) return true;
+    if (rc == CE_OK) return folded;
     const WideArgs wa = wide_args(a);
     const PwPlan pl = pw_plan(a.C);
     const size_t lds = wide_lds_bytes(a.C);
     int rc_excl = CE_OK;
+    bool wide_folded = fold != nullptr;
     rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
         constexpr int DT = decltype(dt)::value, NPL = decltype(npl)::value;
         if constexpr (decltype(vec)::value) {
@@ -74,10 +129,13 @@ bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w,
             rc_excl = CE_EUNSUPPORTED;
             return;
         }
+        sa.ctr = nullptr;  // ... and does not fold
+        wide_folded = false;
         auto kern = k_stream_wide<DT, NPL, decltype(vec)::value>;
         const int grid = resident_grid(kern, lds, G);
         stream_grid(sa, grid);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
     });
-    return rc == CE_OK && rc_excl == CE_OK;
+    if (rc != CE_OK || rc_excl != CE_OK) return 0;
+    return wide_folded ? 2 : 1;
 }

@@ -1,0 +1,366 @@
+// ce_small.hpp -- pools of a few thousand items (BASELINE configs[0..2]: one
+// reference-sized pool, the hc table, the [mc; hc] mix, 500 users in one
+// launch) selected by TILES: a problem (the pool, a user, the mix) is cut into
+// S tiles, one block each, so a 1608-item pool is spread over several CUs
+// instead of one (round 2 ran each problem on one CU).  Every tile computes
+// its items' keys and its own exact top-q; the LAST tile of a problem to
+// finish (an arrival ticket in the workspace) merges the S sorted lists and
+// writes the problem's selection -- still ONE launch, no second kernel.
+//
+// Per tile (amg_test.py:441-445 on the tile's items):
+//   1. the log table's loads are issued, then ALL member loads of the
+//      thread's IPT items (item lo + tid + BS*v: each wave's loads coalesced);
+//      each item's mean + entropy runs as soon as its own loads have landed;
+//   2. the best key of each group of BS/64 lanes (lane-exchange butterfly) ->
+//      64 group bests (distinct items) in LDS; every thread ranks one of them
+//      against a 1/W slice of the others; the group best of rank q-1 is an
+//      exact floor (q items are >= it);
+//   3. items >= the floor are appended to an LDS list (one atomic per wave);
+//      survivor t counts the survivors that beat it and writes itself to slot
+//      `rank` (< q) of the tile's sorted list (or of the final outputs when
+//      S = 1).
+// A tile longer than BS*IPT items (a long user of a ragged batch), or more
+// than 64*W survivors (floods of exact ties at the floor), takes per-wave
+// register lists + a tree merge instead (block-uniform branches, same answer).
+//
+// Merge (S > 1): every thread that wrote list entries fences (release), the
+// block syncs, thread 0 takes a ticket (atomicAdd on the problem's counter);
+// the block that draws S-1 fences (acquire), resets the counter to 0 for the
+// next call, loads the S*q candidates into LDS, and ranks each candidate by
+// its slot in its own list + a binary search in each other list (all lists
+// are best-first; empty slots -- key 0, idx -1 -- sort after every real
+// candidate).  Counters live in the workspace header: zero before the first
+// call (the Python side allocates the workspace zero-filled; ce.h states the
+// contract) and zero again after every call.
+#pragma once
+#include "ce_stream.hpp"
+
+namespace ce {
+
+template <int GS>
+__device__ __forceinline__ void group_best(uint64_t& k, int64_t& i) {
+    uint64_t pk;
+    int64_t pi;
+#define CE_GB(J)                    \
+    if constexpr (GS > J) {         \
+        pk = k;                     \
+        pi = i;                     \
+        xor_cand<J>(pk, pi);        \
+        if (better(pk, pi, k, i)) { \
+            k = pk;                 \
+            i = pi;                 \
+        }                           \
+    }
+    CE_GB(1) CE_GB(2) CE_GB(4) CE_GB(8)
+#undef CE_GB
+}
+
+#ifdef CE_PHASE_TIMING
+// diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
+__device__ uint64_t g_phase[8192][6];
+#define CE_STAMP(b, k) \
+    if (threadIdx.x == 0 && (b) < 8192) g_phase[b][k] = wall_clock64();
+#else
+#define CE_STAMP(b, k)
+#endif
+
+// Geometry of a tiled launch: block b is tile t = b % S of problem p = b / S,
+// S = SA + SB.  Tiles [0, SA) split segment A (committee items: one pool
+// [0, n) or user p's [offsets[p], offsets[p+1])), tiles [SA, S) split segment
+// B (the mix's hc rows [0, nB)).
+struct TileArgs {
+    const int64_t* offsets;  // [P+1] problem offsets (batched users), or nullptr: one problem
+    int64_t n;               // segment-A items (offsets == nullptr)
+    int64_t nB;              // segment-B rows (mix), 0 otherwise
+    int64_t base_idx;        // position of item 0 (offsets == nullptr)
+    int SA, SB;              // tiles per problem over segment A / B
+    Cand* lists;             // [P*S][q] tile lists (S > 1)
+    uint32_t* ctr;           // [P] arrival counters (S > 1): 0 at rest
+};
+
+constexpr int kTileMergeCap = 1024;  // S * q candidates a merge holds (host: S <= kTileMergeCap / q)
+
+template <int WAVES>
+struct TileSmem {
+    static constexpr int CAP = 64 * WAVES;  // one survivor per thread
+    uint64_t gk[64];                        // group bests
+    int64_t gi[64];
+    int part[WAVES][64];                    // partial ranks of the group bests
+    int cnt;                                // survivors appended
+    int ticket;                             // arrival ticket of this tile (S > 1)
+    int nvalid;                             // merge: real candidates over all lists
+    uint64_t ck[CAP];
+    int64_t ci[CAP];
+    union {
+        WaveListsT<WAVES> lists;            // fallback tree merge
+        struct {
+            uint64_t k[kTileMergeCap];
+            int64_t i[kTileMergeCap];
+        } m;                                // the S lists of a problem (merge)
+    };
+};
+
+// Keys of this thread's IPT items lo + tid + BS*v of [lo, hi) (all loads in
+// flight before the arithmetic; `tab` committed once the data is awaited).
+template <class Src, int IPT, int UNR, int BS, int K>
+__device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi, int64_t rel, const uint32_t* excl,
+                                          LogTablePrefetch& tab, uint64_t (&k)[K], int64_t (&pos)[K],
+                                          bool (&ok)[K]) {
+    static_assert(IPT <= K, "");
+    const int tid = threadIdx.x, w = tid >> 6;
+    const int64_t len = hi - lo;
+    int64_t items[IPT];
+    uint64_t kk[IPT];
+    int nlive = 0;  // this wave's item slots holding at least one real item (a prefix)
+#pragma unroll
+    for (int v = 0; v < IPT; ++v) {
+        const int64_t j = tid + (int64_t)BS * v;
+        items[v] = lo + (j < len ? j : (len > 0 ? len - 1 : 0));
+        kk[v] = 0;
+        nlive += (int64_t)BS * v + 64 * w < len;
+    }
+    if (len > 0) {  // block-uniform
+        src.template keys_small<UNR, IPT>(items, kk, nlive, [&]() { tab.commit(); });
+    } else {
+        tab.commit();
+    }
+#pragma unroll
+    for (int v = 0; v < K; ++v) {
+        if (v < IPT) {
+            k[v] = kk[v];
+            pos[v] = items[v] + rel;
+            ok[v] = tid + (int64_t)BS * v < len;
+            if (excl) ok[v] = ok[v] && !excluded(excl, items[v]);
+        } else {
+            k[v] = 0;
+            pos[v] = INT64_MAX;
+            ok[v] = false;
+        }
+    }
+}
+
+template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_select_tiles(
+    SrcA srcA, SrcB srcB, TileArgs ta, int q, double* __restrict__ oval, int64_t* __restrict__ oidx,
+    const uint32_t* __restrict__ excl) {
+    constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
+    constexpr int K = IPTA > IPTB ? IPTA : IPTB;
+    static_assert(BS % 64 == 0 && BS >= 128 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
+    using SM = TileSmem<W>;
+    __shared__ SM sm;
+    CE_STAMP(blockIdx.x, 0)
+    LogTablePrefetch tab;
+    tab.fetch();
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int S = ta.SA + ta.SB;
+    const int p = blockIdx.x / S, t = blockIdx.x - p * S;
+    const int64_t s0 = ta.offsets ? ta.offsets[p] : 0, s1 = ta.offsets ? ta.offsets[p + 1] : ta.n;
+    const int64_t lenA = s1 > s0 ? s1 - s0 : 0;
+    const int64_t rel = (ta.offsets ? 0 : ta.base_idx) - s0;  // A: position = item + rel
+    const int64_t relB = ta.n + ta.base_idx;                  // B: position = row + relB
+    const bool segB = IPTB > 0 && t >= ta.SA;                 // block-uniform
+    int64_t lo, hi;
+    if (!segB) {
+        const int64_t per = (lenA + ta.SA - 1) / ta.SA;
+        lo = s0 + (int64_t)t * per;
+        hi = lo + per < s1 ? lo + per : s1;
+    } else {
+        const int64_t per = (ta.nB + ta.SB - 1) / ta.SB;
+        lo = (int64_t)(t - ta.SA) * per;
+        hi = lo + per < ta.nB ? lo + per : ta.nB;
+    }
+    if (lo > hi) lo = hi;
+    const bool direct = S == 1;  // the tile is the whole problem: final outputs, no merge
+    double* ov = oval + (int64_t)p * q;
+    int64_t* oi = oidx + (int64_t)p * q;
+    Cand* lst = ta.lists + (int64_t)blockIdx.x * q;
+    CE_DASSERT(q >= 1 && q <= 64);
+    CE_DASSERT(direct || (int64_t)S * q <= kTileMergeCap);
+
+    if (hi - lo > (int64_t)BS * (segB ? IPTB : IPTA)) {  // long tile: per-wave streams + tree merge
+        tab.commit();
+        constexpr int64_t kIt = 64 * 2;
+        RegTopQ tq;
+        tq.init(q);
+        const int64_t its = (hi - lo + kIt - 1) / kIt, its_w = (its + W - 1) / W;
+        int64_t wlo = lo + (int64_t)w * its_w * kIt;
+        int64_t whi = wlo + its_w * kIt < hi ? wlo + its_w * kIt : hi;
+        if (wlo > whi) wlo = whi;
+        if (!segB) {
+            stream_direct_range<SrcA, 2, UNRA>(srcA, wlo, whi, rel, q, tq, excl);
+        } else {
+            if constexpr (IPTB > 0) stream_direct_range<SrcB, 2, UNRB>(srcB, wlo, whi, relB, q, tq, nullptr);
+        }
+        if (direct) {
+            block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
+            return;
+        }
+        block_merge_write<W>(tq, sm.lists, q, lst, 0);
+    } else {
+        // 1. keys of this thread's items
+        uint64_t k[K];
+        int64_t pos[K];
+        bool ok[K];
+        if (!segB) {
+            tile_keys<SrcA, IPTA, UNRA, BS, K>(srcA, lo, hi, rel, excl, tab, k, pos, ok);
+        } else {
+            if constexpr (IPTB > 0) tile_keys<SrcB, IPTB, UNRB, BS, K>(srcB, lo, hi, relB, nullptr, tab, k, pos, ok);
+        }
+        CE_STAMP(blockIdx.x, 1)
+        uint64_t bk = 0;
+        int64_t bi = INT64_MAX;
+#pragma unroll
+        for (int v = 0; v < K; ++v)
+            if (ok[v] && better(k[v], pos[v], bk, bi)) {
+                bk = k[v];
+                bi = pos[v];
+            }
+        // 2. floor = the group best of rank q-1 (ranks split over the waves)
+        group_best<GS>(bk, bi);
+        if ((tid & (GS - 1)) == 0) {
+            sm.gk[tid / GS] = bk;
+            sm.gi[tid / GS] = bi;
+        }
+        if (tid == 0) sm.cnt = 0;
+        __syncthreads();
+        {
+            const uint64_t mk = sm.gk[lane];
+            const int64_t mi = sm.gi[lane];
+            int r = 0;
+#pragma unroll
+            for (int j = 0; j < 64 / W; ++j) {
+                const int o = w * (64 / W) + j;
+                r += better(sm.gk[o], sm.gi[o], mk, mi);
+            }
+            sm.part[w][lane] = r;
+        }
+        __syncthreads();
+        uint64_t fk = 0;  // no group best of rank q-1 (fewer valid groups): admit every valid item
+        int64_t fi = INT64_MAX;
+        {
+            int r = 0;
+#pragma unroll
+            for (int j = 0; j < W; ++j) r += sm.part[j][lane];
+            const uint64_t hit = __ballot(r == q - 1);
+            if (hit) {
+                const int sl = __builtin_ctzll(hit);
+                fk = sm.gk[sl];
+                fi = sm.gi[sl];
+            }
+        }
+        CE_STAMP(blockIdx.x, 2)
+        // 3. survivors (not worse than the floor) -> LDS list
+#pragma unroll
+        for (int v = 0; v < K; ++v) {
+            const bool pass = ok[v] && !better(fk, fi, k[v], pos[v]);
+            const uint64_t m = __ballot(pass);
+            if (m) {  // wave-uniform
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&sm.cnt, __popcll(m));
+                base = __builtin_amdgcn_readfirstlane(base);
+                const int slot =
+                    base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (pass && slot < SM::CAP) {
+                    sm.ck[slot] = k[v];
+                    sm.ci[slot] = pos[v];
+                }
+            }
+        }
+        __syncthreads();
+        CE_STAMP(blockIdx.x, 3)
+        const int nc = sm.cnt;
+        if (nc <= SM::CAP) {
+            if (tid < nc) {  // survivor tid takes the slot of its rank
+                const uint64_t mk = sm.ck[tid];
+                const int64_t mi = sm.ci[tid];
+                int r = 0;
+                for (int j = 0; j < nc; ++j) r += better(sm.ck[j], sm.ci[j], mk, mi);
+                if (r < q) {
+                    if (direct) {
+                        ov[r] = key_to_val(mk);
+                        oi[r] = mi;
+                    } else {
+                        lst[r] = Cand{mk, mi};
+                    }
+                }
+            } else if (tid < q) {  // fewer survivors than q: padding
+                if (direct) {
+                    ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
+                    oi[tid] = -1;
+                } else {
+                    lst[tid] = Cand{0ull, -1};
+                }
+            }
+            CE_STAMP(blockIdx.x, 4)
+            if (direct) return;
+        } else {
+            // overflow (> CAP items tie at or above the floor): per-wave lists + tree merge
+            RegTopQ tq;
+            tq.init(q, fk, fi == INT64_MAX ? fi : fi + 1);  // admit candidates >= the floor
+#pragma unroll
+            for (int v = 0; v < K; ++v) tq.offer(k[v], pos[v], ok[v]);
+            if (direct) {
+                block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
+                return;
+            }
+            block_merge_write<W>(tq, sm.lists, q, lst, 0);
+        }
+    }
+
+    // ---- arrival ticket: the last tile of problem p merges the S lists ----
+    __threadfence();  // release this tile's list (every writer fences its own stores)
+    __syncthreads();
+    if (tid == 0) sm.ticket = (int)atomicAdd(&ta.ctr[p], 1u);
+    __syncthreads();
+    const int ticket = sm.ticket;
+    CE_DASSERT(ticket >= 0 && ticket < S);
+    if (ticket != S - 1) return;  // block-uniform
+    __threadfence();              // acquire: every other tile's list is visible
+    if (tid == 0) {
+        atomicExch(&ta.ctr[p], 0u);  // every tile of p has arrived: reset for the next call
+        sm.nvalid = 0;
+    }
+    const Cand* L = ta.lists + (int64_t)p * S * q;
+    const int nL = S * q;
+    for (int j = tid; j < nL; j += BS) {
+        const Cand c = L[j];
+        sm.m.k[j] = c.key;
+        sm.m.i[j] = c.idx;
+    }
+    __syncthreads();
+    for (int j0 = 0; j0 < nL; j0 += BS) {  // block-uniform bound
+        const int j = j0 + tid;
+        const bool valid = j < nL && sm.m.i[j] >= 0;
+        const uint64_t vm = __ballot(valid);
+        if (lane == 0 && vm) atomicAdd(&sm.nvalid, __popcll(vm));
+        if (valid) {
+            const uint64_t ck = sm.m.k[j];
+            const int64_t cidx = sm.m.i[j];
+            const int a = j / q;
+            int rank = j - a * q;  // its slot in its own list
+            for (int b = 0; b < S; ++b) {
+                if (b == a) continue;
+                // entries of list b better than (ck, cidx): a prefix of the list
+                int l = 0, h = q;
+                while (l < h) {
+                    const int mid = (l + h) >> 1;
+                    if (better(sm.m.k[b * q + mid], sm.m.i[b * q + mid], ck, cidx)) l = mid + 1;
+                    else h = mid;
+                }
+                rank += l;
+            }
+            if (rank < q) {
+                ov[rank] = key_to_val(ck);
+                oi[rank] = cidx;
+            }
+        }
+    }
+    __syncthreads();
+    for (int r = sm.nvalid + tid; r < q; r += BS) {  // fewer real candidates than q: padding
+        ov[r] = __longlong_as_double(0x7ff8000000000000ll);
+        oi[r] = -1;
+    }
+    CE_STAMP(blockIdx.x, 5)
+}
+
+}  // namespace ce

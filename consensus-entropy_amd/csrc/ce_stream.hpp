@@ -266,6 +266,37 @@ struct ItemTile {
         }
     }
 
+    // Member-major [M, N, C] (the reference's stack np.array(pred_prob),
+    // amg_test.py:441) with 16-B member rows (C * elem = 16): the tile is S = M
+    // contiguous 1 KiB runs, member k's 64 items at lds + k*1024 -- one
+    // LDS-DMA per member, no swizzle (lane l reads bytes l*16.. of each run:
+    // 16 lanes of a ds_read_b128 group hit 16 distinct bank groups).
+    template <int AUX>
+    __device__ __forceinline__ static void issue_mnc(const char* base, int64_t t0, int n_valid, int64_t sMb,
+                                                     char* lds) {
+        const int lane = threadIdx.x & 63;
+        const int64_t it = t0 + (lane < n_valid ? lane : n_valid - 1);
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const char* src = base + (int64_t)k * sMb + it * 16;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)src, (void __attribute__((address_space(3)))*)(lds + k * 1024), 16, 0, AUX);
+        }
+    }
+
+    __device__ __forceinline__ void read_mnc(const char* lds) {
+        const int lane = threadIdx.x & 63;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int m = 0; m < S; ++m) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(lds + m * 1024 + lane * 16);
+            u[4 * m + 0] = v.x;
+            u[4 * m + 1] = v.y;
+            u[4 * m + 2] = v.z;
+            u[4 * m + 3] = v.w;
+        }
+    }
+
     __device__ __forceinline__ void read(const char* lds) {
         const int lane = threadIdx.x & 63;
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -335,6 +366,12 @@ struct StreamArgs {
     int64_t per_wave;  // items per wave (multiple of 64)
     const uint32_t* excl;  // exclusion bitmap over items 0..N-1 (1 = out of the pool), or nullptr
     int nlists;        // workspace lists (>= gridDim.x); lists past the grid are written empty
+    // stage 2 folded in (ctr != nullptr): the last block merges the grid's
+    // lists into (oval, oidx), or into q records at ocand
+    uint32_t* ctr;
+    double* oval;
+    int64_t* oidx;
+    Cand* ocand;
 };
 
 // Merge the block's WAVES wave lists (registers, best-first) into the
@@ -383,10 +420,109 @@ __device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L
     }
 }
 
-// Item-major, dense rows of 16*S bytes, LDS-DMA staged (AUX: DMA cache policy).
-template <int DT, int C, int S, int AUX>
+// A source of best-first candidate lists: Cand records (the workspace, the
+// ranks' all-gathered records) or (val, idx) arrays (ce_topq_merge).
+template <bool FROM_VALS>
+struct ListSrc {
+    const Cand* c;
+    const double* val;
+    const int64_t* idx;
+    __device__ __forceinline__ void get(int64_t j, uint64_t& k, int64_t& i) const {
+        if constexpr (FROM_VALS) {
+            i = idx[j];
+            k = order_key(val[j]);
+        } else {
+            const Cand x = c[j];
+            k = x.key;
+            i = x.idx;
+        }
+    }
+};
+
+// Merge nl best-first lists of q candidates (empty slots, idx < 0, at each
+// list's tail) with the W waves of ONE block into the top-q, written as final
+// (oval, oidx) or as records (ocand).  Exact floor from the list heads: the
+// q-th best head T_w among a wave's lists is reached by q distinct lists, so
+// every global top-q candidate is >= T = the best T_w; only lists whose head
+// is >= T (~q of them) are read past their head, and only their entries >= T
+// enter the register lists.  One round of head loads (nl / (64 W) per lane)
+// plus ~q list loads per block instead of all nl * q candidates.
+// bk / bi: W-entry LDS scratch; L: the block-merge scratch.
+template <int W, bool FROM_VALS>
+__device__ inline void merge_lists_block(ListSrc<FROM_VALS> src, int64_t seg0, int nl, int q, WaveListsT<W>& L,
+                                         uint64_t* bk, int64_t* bi, double* oval, int64_t* oidx, Cand* ocand) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    RegTopQ hq;
+    hq.init(q);
+    for (int g0 = w * 64; g0 < nl; g0 += W * 64) {
+        const int g = g0 + lane;
+        uint64_t hk = 0;
+        int64_t hid = -1;
+        src.get(seg0 + (int64_t)(g < nl ? g : nl - 1) * q, hk, hid);  // clamped: no branch around a load
+        hq.offer(hk, hid, g < nl && hid >= 0);
+    }
+    if (lane == 0) {
+        bk[w] = readlane64(hq.k, q - 1);
+        bi[w] = (int64_t)readlane64((uint64_t)hq.i, q - 1);
+    }
+    __syncthreads();
+    uint64_t fk = 0;
+    int64_t fi = INT64_MAX;
+    for (int v = 0; v < W; ++v)
+        if (bi[v] != INT64_MAX && better(bk[v], bi[v], fk, fi)) {
+            fk = bk[v];
+            fi = bi[v];
+        }
+    if (fi != INT64_MAX) fi += 1;  // admit candidates >= T: strictly better than (T.key, T.idx + 1)
+    RegTopQ tq;
+    tq.init(q, fk, fi);
+    for (int g0 = w * 64; g0 < nl; g0 += W * 64) {
+        const int g = g0 + lane;
+        uint64_t hk = 0;
+        int64_t hid = -1;
+        src.get(seg0 + (int64_t)(g < nl ? g : nl - 1) * q, hk, hid);  // L1/L2-hot: read in phase 1
+        uint64_t m = __ballot(g < nl && hid >= 0 && better(hk, hid, fk, fi));
+        while (m) {  // wave-uniform: each list whose head reaches the floor
+            const int s = __builtin_ctzll(m);
+            m &= m - 1;
+            const int64_t base = seg0 + (int64_t)(g0 + s) * q;
+            uint64_t ck = 0;
+            int64_t ci = -1;
+            src.get(base + (lane < q ? lane : q - 1), ck, ci);
+            tq.offer(ck, ci, lane < q && ci >= 0);
+        }
+    }
+    block_merge_write<W>(tq, L, q, ocand, 0, ocand ? nullptr : oval, oidx);
+}
+
+// Arrival ticket of a stage-1 grid (a.ctr != nullptr: stage 2 folded into
+// stage 1): after its list is written, every block fences (release) and
+// takes a ticket; the block that draws gridDim.x - 1 fences (acquire), resets
+// the counter and merges the grid's lists into the final output / records.
+template <int W>
+__device__ inline void fold_merge(const StreamArgs& a, int q, const Cand* wc0, WaveListsT<W>& L) {
+    __shared__ int ticket;
+    __shared__ uint64_t bk[W];
+    __shared__ int64_t bi[W];
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) ticket = (int)atomicAdd(a.ctr, 1u);
+    __syncthreads();
+    CE_DASSERT(ticket >= 0 && ticket < (int)gridDim.x);
+    if (ticket != (int)gridDim.x - 1) return;  // block-uniform
+    __threadfence();
+    if (threadIdx.x == 0) atomicExch(a.ctr, 0u);
+    merge_lists_block<W, false>(ListSrc<false>{wc0, nullptr, nullptr}, 0, gridDim.x, q, L, bk, bi, a.oval, a.oidx,
+                                a.ocand);
+}
+
+// Item-major, dense rows of 16*S bytes, LDS-DMA staged (AUX: DMA cache policy);
+// MNC: the member-major stack with 16-B member rows instead (S = M members,
+// member stride a.sM elements).
+template <int DT, int C, int S, int AUX, bool MNC = false>
 __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    CE_DASSERT((int)gridDim.x <= a.nlists && q >= 1 && q <= kStreamMaxQ);
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
@@ -398,15 +534,22 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     tq.init(q);
     const char* base = static_cast<const char*>(a.p);
     char* lds = sm.tile[w];
+    constexpr int EB = DT == kF64 ? 8 : (DT == kF32 ? 4 : 2);
+    const int64_t sMb = a.sM * EB;
+    auto issue = [&](int64_t t, int nv) {
+        if constexpr (MNC) ItemTile<S>::template issue_mnc<AUX>(base, t, nv, sMb, lds);
+        else ItemTile<S>::template issue<AUX>(base, t, nv, lds);
+    };
     ItemTile<S> t;
-    if (lo < hi) ItemTile<S>::template issue<AUX>(base, lo, (int)min<int64_t>(64, hi - lo), lds);
+    if (lo < hi) issue(lo, (int)min<int64_t>(64, hi - lo));
     for (int64_t t0 = lo; t0 < hi; t0 += 64) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        t.read(lds);
+        if constexpr (MNC) t.read_mnc(lds);
+        else t.read(lds);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         const int64_t t1 = t0 + 64;
-        if (t1 < hi) ItemTile<S>::template issue<AUX>(base, t1, (int)min<int64_t>(64, hi - t1), lds);
+        if (t1 < hi) issue(t1, (int)min<int64_t>(64, hi - t1));
         double mean[C];
         t.template mean<DT, C>(a.dM, a.invM, a.pow2, mean);
         const double h = entropy_row<C>(mean);
@@ -416,6 +559,7 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
         tq.offer(order_key(h), i + a.base_idx, ok);
     }
     block_merge_write<4>(tq, sm.lists, q, wc + (int64_t)blockIdx.x * q, a.nlists);
+    if (a.ctr) fold_merge<4>(a, q, wc, sm.lists);
 }
 
 // Any strides (vector loads when aligned): member-major [M, N, C] streams
@@ -447,6 +591,7 @@ __device__ __forceinline__ void stream_direct_range(const Src& src, int64_t lo, 
 template <class Src, int IPL, int UNR>
 __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, int q, Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    CE_DASSERT((int)gridDim.x <= a.nlists && q >= 1 && q <= kStreamMaxQ);
     __shared__ WaveLists sm;
     const int w = threadIdx.x >> 6;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
@@ -458,6 +603,7 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     tq.init(q);
     stream_direct_range<Src, IPL, UNR>(src, lo, hi, a.base_idx, q, tq, a.excl);
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists);
+    if (a.ctr) fold_merge<4>(a, q, wc, sm);
 }
 
 // Batched pools (amg_test.py:345's per-user loop in one launch): user u owns
@@ -561,247 +707,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_stream_seg(Src src, const int64_
     } else {
         block_merge_write<WAVES>(tq, sm, q, wc + (int64_t)blockIdx.x * q, 0, nullptr, nullptr, nw);
     }
-}
-
-// ---------------------------------------------------------------------------
-// Small pools in ONE block each (the per-user loop of amg_test.py:345 around
-// :441-445 in one launch; also a single pool of <= BS*IPT items): no second
-// launch, no per-wave lists, no tree merge, no sort network.
-//   1. the log table's loads are issued, then ALL member loads of the
-//      thread's IPT items (item tid + BS*v: each wave's loads coalesced); the
-//      table reaches LDS while the data is awaited anyway;
-//   2. the best key of each group of BS/64 lanes (lane-exchange butterfly) ->
-//      64 group bests (distinct items) in LDS; every thread ranks one of them
-//      against a 1/W slice of the others, and the group best of rank q-1 is
-//      the floor: q items are >= it, so only items >= the floor can be
-//      selected (exact);
-//   3. items >= the floor are appended to an LDS list (one atomic per wave);
-//      survivor t (usually ~q of them) counts the survivors that beat it and
-//      writes itself to output slot `rank` if rank < q.
-// A pool longer than BS*IPT, or more than CAP survivors (masses of exact ties
-// at the floor), takes per-wave register lists + a tree merge instead
-// (block-uniform branches, same answer).
-// offsets == nullptr: one pool [0, n) with positions base_idx + i; else block u
-// is user u, positions user-local.  excl: exclusion bitmap, or nullptr.
-// ---------------------------------------------------------------------------
-template <int GS>
-__device__ __forceinline__ void group_best(uint64_t& k, int64_t& i) {
-    uint64_t pk;
-    int64_t pi;
-#define CE_GB(J)                    \
-    if constexpr (GS > J) {         \
-        pk = k;                     \
-        pi = i;                     \
-        xor_cand<J>(pk, pi);        \
-        if (better(pk, pi, k, i)) { \
-            k = pk;                 \
-            i = pi;                 \
-        }                           \
-    }
-    CE_GB(1) CE_GB(2) CE_GB(4) CE_GB(8)
-#undef CE_GB
-}
-
-#ifdef CE_PHASE_TIMING
-// diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
-__device__ uint64_t g_phase[4096][6];
-#define CE_STAMP(b, k) \
-    if (threadIdx.x == 0 && (b) < 4096) g_phase[b][k] = wall_clock64();
-#else
-#define CE_STAMP(b, k)
-#endif
-
-template <int WAVES>
-struct SmallSmem {
-    static constexpr int CAP = 64 * WAVES;  // one survivor per thread
-    uint64_t gk[64];                        // group bests
-    int64_t gi[64];
-    int part[WAVES][64];                    // partial ranks of the group bests
-    int cnt;                                // survivors appended
-    uint64_t ck[CAP];
-    int64_t ci[CAP];
-    WaveListsT<WAVES> lists;                // fallback tree merge
-};
-
-// Two segments in one block (SrcB, IPTB > 0: the mix of amg_test.py:473-480,
-// committee items then hc rows): segment A's items keep positions item + rel,
-// segment B's rows [0, nB) follow at n + base_idx + j; one selection over both.
-template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_select_small(
-    SrcA srcA, SrcB srcB, const int64_t* __restrict__ offsets, int64_t n, int64_t nB, int64_t base_idx, int q,
-    double* __restrict__ oval, int64_t* __restrict__ oidx, const uint32_t* __restrict__ excl) {
-    constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
-    constexpr int K = IPTA + IPTB, IB = IPTB > 0 ? IPTB : 1;
-    static_assert(BS % 64 == 0 && BS >= 256 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
-    using SM = SmallSmem<W>;
-    __shared__ SM sm;
-    CE_STAMP(blockIdx.x, 0)
-    LogTablePrefetch tab;
-    tab.fetch();
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int u = blockIdx.x;
-    const int64_t s0 = offsets ? offsets[u] : 0, s1 = offsets ? offsets[u + 1] : n;
-    const int64_t len = s1 > s0 ? s1 - s0 : 0;
-    const int64_t rel = (offsets ? 0 : base_idx) - s0;  // position = item + rel
-    const int64_t relB = n + base_idx;                  // segment B: position = row + relB
-    if constexpr (IPTB == 0) nB = 0;
-    double* ov = oval + (int64_t)u * q;
-    int64_t* oi = oidx + (int64_t)u * q;
-    if (len > (int64_t)BS * IPTA || nB > (int64_t)BS * IPTB) {  // long pools: per-wave streams + tree merge
-        tab.commit();
-        constexpr int64_t kIt = 64 * 2;
-        RegTopQ tq;
-        tq.init(q);
-        {
-            const int64_t its = (len + kIt - 1) / kIt, its_w = (its + W - 1) / W;
-            int64_t lo = s0 + (int64_t)w * its_w * kIt;
-            int64_t hi = lo + its_w * kIt < s1 ? lo + its_w * kIt : s1;
-            if (lo > hi) lo = hi;
-            stream_direct_range<SrcA, 2, UNRA>(srcA, lo, hi, rel, q, tq, excl);
-        }
-        if constexpr (IPTB > 0) {
-            const int64_t its = (nB + kIt - 1) / kIt, its_w = (its + W - 1) / W;
-            int64_t lo = (int64_t)w * its_w * kIt;
-            int64_t hi = lo + its_w * kIt < nB ? lo + its_w * kIt : nB;
-            if (lo > hi) lo = hi;
-            stream_direct_range<SrcB, 2, UNRB>(srcB, lo, hi, relB, q, tq, nullptr);
-        }
-        block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
-        return;
-    }
-    // 1. keys of this thread's items, every load of a segment in flight before its math
-    uint64_t k[K];
-    int64_t pos[K];
-    bool ok[K];
-    {
-        int64_t items[IPTA];
-        uint64_t ka[IPTA];
-        int nlive = 0;  // this wave's item slots holding at least one real item (a prefix)
-#pragma unroll
-        for (int v = 0; v < IPTA; ++v) {
-            const int64_t j = tid + (int64_t)BS * v;
-            items[v] = s0 + (j < len ? j : (len > 0 ? len - 1 : 0));
-            ka[v] = 0;
-            nlive += (int64_t)BS * v + 64 * w < len;
-        }
-        if (len > 0) {  // block-uniform
-            srcA.template keys_small<UNRA, IPTA>(items, ka, nlive, [&]() { tab.commit(); });
-        } else {
-            tab.commit();
-        }
-#pragma unroll
-        for (int v = 0; v < IPTA; ++v) {
-            k[v] = ka[v];
-            pos[v] = items[v] + rel;
-            ok[v] = tid + (int64_t)BS * v < len;
-            if (excl) ok[v] = ok[v] && !excluded(excl, items[v]);
-        }
-    }
-    if constexpr (IPTB > 0) {
-        int64_t rows[IB];
-        uint64_t kb[IB];
-        int nlive = 0;
-#pragma unroll
-        for (int v = 0; v < IPTB; ++v) {
-            const int64_t j = tid + (int64_t)BS * v;
-            rows[v] = j < nB ? j : (nB > 0 ? nB - 1 : 0);
-            kb[v] = 0;
-            nlive += (int64_t)BS * v + 64 * w < nB;
-        }
-        if (nB > 0) srcB.template keys_small<UNRB, IPTB>(rows, kb, nlive);
-#pragma unroll
-        for (int v = 0; v < IPTB; ++v) {
-            k[IPTA + v] = kb[v];
-            pos[IPTA + v] = rows[v] + relB;
-            ok[IPTA + v] = tid + (int64_t)BS * v < nB;
-        }
-    }
-    CE_STAMP(u, 1)
-    uint64_t bk = 0;
-    int64_t bi = INT64_MAX;
-#pragma unroll
-    for (int v = 0; v < K; ++v)
-        if (ok[v] && better(k[v], pos[v], bk, bi)) {
-            bk = k[v];
-            bi = pos[v];
-        }
-    // 2. floor = the group best of rank q-1 (ranks split over the waves)
-    group_best<GS>(bk, bi);
-    if ((tid & (GS - 1)) == 0) {
-        sm.gk[tid / GS] = bk;
-        sm.gi[tid / GS] = bi;
-    }
-    if (tid == 0) sm.cnt = 0;
-    __syncthreads();
-    {
-        const uint64_t mk = sm.gk[lane];
-        const int64_t mi = sm.gi[lane];
-        int r = 0;
-#pragma unroll
-        for (int j = 0; j < 64 / W; ++j) {
-            const int o = w * (64 / W) + j;
-            r += better(sm.gk[o], sm.gi[o], mk, mi);
-        }
-        sm.part[w][lane] = r;
-    }
-    __syncthreads();
-    uint64_t fk = 0;  // no group best of rank q-1 (fewer valid groups): admit every valid item
-    int64_t fi = INT64_MAX;
-    {
-        int r = 0;
-#pragma unroll
-        for (int j = 0; j < W; ++j) r += sm.part[j][lane];
-        const uint64_t hit = __ballot(r == q - 1);
-        if (hit) {
-            const int sl = __builtin_ctzll(hit);
-            fk = sm.gk[sl];
-            fi = sm.gi[sl];
-        }
-    }
-    CE_STAMP(u, 2)
-    // 3. survivors (not worse than the floor) -> LDS list
-#pragma unroll
-    for (int v = 0; v < K; ++v) {
-        const bool pass = ok[v] && !better(fk, fi, k[v], pos[v]);
-        const uint64_t m = __ballot(pass);
-        if (m) {  // wave-uniform
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&sm.cnt, __popcll(m));
-            base = __builtin_amdgcn_readfirstlane(base);
-            const int slot =
-                base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            if (pass && slot < SM::CAP) {
-                sm.ck[slot] = k[v];
-                sm.ci[slot] = pos[v];
-            }
-        }
-    }
-    __syncthreads();
-    CE_STAMP(u, 3)
-    const int nc = sm.cnt;
-    if (nc <= SM::CAP) {
-        if (tid < nc) {  // survivor tid takes the output slot of its rank
-            const uint64_t mk = sm.ck[tid];
-            const int64_t mi = sm.ci[tid];
-            int r = 0;
-            for (int j = 0; j < nc; ++j) r += better(sm.ck[j], sm.ci[j], mk, mi);
-            if (r < q) {
-                ov[r] = key_to_val(mk);
-                oi[r] = mi;
-            }
-        } else if (tid < q) {  // fewer survivors than q: padding
-            ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
-            oi[tid] = -1;
-        }
-        CE_STAMP(u, 4)
-        return;
-    }
-    // overflow (> CAP items tie at or above the floor): per-wave lists + tree merge
-    RegTopQ tq;
-    tq.init(q, fk, fi == INT64_MAX ? fi : fi + 1);  // admit candidates >= the floor
-#pragma unroll
-    for (int v = 0; v < K; ++v) tq.offer(k[v], pos[v], ok[v]);
-    block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
 }
 
 }  // namespace ce

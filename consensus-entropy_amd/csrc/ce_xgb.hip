@@ -36,6 +36,8 @@
 // lane.  Bound: latency of those chains (X bytes from HBM, D * sizeof(x) per
 // frame, are read once; T * d node steps per frame).
 #include <hip/hip_runtime.h>
+
+#include "ce_debug.hpp"
 #include <stdint.h>
 
 #include <algorithm>
@@ -188,6 +190,7 @@ struct WalkForest {
     const float* leaves;  // [T][NI + 1]
     const int32_t* goff;  // [G + 1]
     int depth, NI;
+    int goff_end;         // T = goff[G] trees (debug bounds checks only)
 
     template <bool MISS>
     static __device__ __forceinline__ bool go_right(uint2 nd, const float* xs, int D, int lane) {
@@ -226,12 +229,18 @@ struct WalkForest {
             // bound by the texture path's address rate: TA 79 % busy; 4M frames
             // 5.45 -> 4.88 ms).  Level 2 the same way (4 nodes, two selects) was
             // slower (5.18 ms): the extra VALU outweighs the saved gather.
-            uint4 p1[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) p1[j] = *reinterpret_cast<const uint4*>(tn[j] + 1);
+            // nodes 1 and 2 as two 8-B loads: a tree holds 2^d - 1 nodes (odd), so
+            // node 1 of every other tree is only 8-byte aligned (the compiler
+            // still merges the pair into one scalar load where it can)
+            uint2 n1[8], n2[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const uint2 nd = idx[j] == 1 ? uint2{p1[j].x, p1[j].y} : uint2{p1[j].z, p1[j].w};
+                n1[j] = tn[j][1];
+                n2[j] = tn[j][2];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint2 nd = idx[j] == 1 ? n1[j] : n2[j];
                 idx[j] = 2 * idx[j] + 1 + (go_right<MISS>(nd, xs, D, lane) ? 1 : 0);
             }
             lev0 = 2;
@@ -239,15 +248,24 @@ struct WalkForest {
         for (int lev = lev0; lev < depth; ++lev) {
             uint2 nd[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) nd[j] = tn[j][idx[j]];
+            for (int j = 0; j < 8; ++j) {
+                CE_DASSERT(idx[j] >= 0 && idx[j] < NI);  // an inner node
+                nd[j] = tn[j][idx[j]];
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) idx[j] = 2 * idx[j] + 1 + (go_right<MISS>(nd[j], xs, D, lane) ? 1 : 0);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) li[j] = idx[j] - NI;
+        for (int j = 0; j < 8; ++j) {
+            li[j] = idx[j] - NI;
+            CE_DASSERT(li[j] >= 0 && li[j] <= NI);  // a leaf of a perfect tree of depth `depth`
+        }
     }
     // leaf value of tree t at leaf index li
-    __device__ __forceinline__ float value(int t, int li) const { return leaves[(int64_t)t * (NI + 1) + li]; }
+    __device__ __forceinline__ float value(int t, int li) const {
+        CE_DASSERT(t >= 0 && t < goff_end && li >= 0 && li <= NI);
+        return leaves[(int64_t)t * (NI + 1) + li];
+    }
 };
 
 // ---- one block per 64-frame tile: G x S waves ------------------------------
@@ -349,7 +367,12 @@ template <int XDT, int ODT>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_xgb_walk(XgbArgs a, const uint2* __restrict__ nodes,
                                                    const float* __restrict__ leaves, const int32_t* __restrict__ goff,
                                                    int depth) {
-    xgb_tile<XDT, ODT>(a, WalkForest{nodes, leaves, goff, depth, (1 << depth) - 1});
+#ifdef CE_DEBUG
+    const int T = goff[a.G];
+#else
+    const int T = 0;
+#endif
+    xgb_tile<XDT, ODT>(a, WalkForest{nodes, leaves, goff, depth, (1 << depth) - 1, T});
 }
 
 __global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict__ y) {

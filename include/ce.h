@@ -13,7 +13,12 @@
  *   - every call is stream-ordered on `stream` (a hipStream_t; NULL = legacy
  *     default stream) and asynchronous: nothing is read back to the host;
  *   - nothing allocates: scratch comes from the caller's `ws`, sized by the
- *     matching *_workspace_bytes() function (pure host arithmetic);
+ *     matching *_workspace_bytes() function (pure host arithmetic).  A
+ *     workspace must be ZERO-FILLED before its first use (e.g. hipMemsetAsync
+ *     once after allocating it): its 64 KiB header holds the arrival counters
+ *     of the tiled kernels (a block that finishes last merges its problem's
+ *     tiles), and every call leaves them zero again, so one workspace serves
+ *     any sequence of calls on one stream;
  *   - return 0 (CE_OK) or a negative CE_E* code; ce_last_error() gives a
  *     thread-local message.  Nothing throws across the ABI;
  *   - strides are in ELEMENTS.  Element (n, m, c) of a committee tensor lives at
@@ -182,7 +187,9 @@ int ce_topq_merge(const double *vals, const int64_t *idx, int32_t nlists, int32_
 /*
  * Fused mc selection -- replaces amg_test.py:441-445 in one pass over the
  * committee tensor (entropies never reach HBM): scores each item and keeps a
- * per-block top-q in LDS, then merges the blocks' candidates.
+ * per-block top-q, then merges the blocks' candidates -- for q <= 64 inside
+ * the same launch (the last block to finish merges), so the whole selection
+ * is one kernel.
  * ce_select_mc_partial + ce_topq_merge_ws are the same two stages exposed
  * separately (the multi-GPU driver and the bench time them apart).
  */
@@ -218,6 +225,11 @@ typedef struct {
 
 int ce_select_finish_cands(int64_t N, int32_t q, void *ws, size_t ws_bytes, ce_cand *out,
                            ce_stream_t stream);
+/* ce_select_mc writing the pool's q records to `out` in ONE launch (stage 2
+ * folded into stage 1's last block; ws sized by ce_select_mc_workspace_bytes). */
+int ce_select_mc_cands(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
+                       int64_t sM, int64_t sC, int32_t q, int64_t base_idx, void *ws, size_t ws_bytes,
+                       ce_cand *out, ce_stream_t stream);
 int ce_merge_cands(const ce_cand *c, int32_t nlists, int32_t q, double *val_out, int64_t *idx_out,
                    ce_stream_t stream);
 

@@ -107,6 +107,45 @@ def test_sharded_records_equal_global(world, N, q):
         assert all(x == -1 for x in list(i)[len(ig):])
 
 
+def _worker_dead_rank(rank, world, port, out):
+    import sys
+    import time
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "consensus-entropy_amd"))
+    from ce_amd import dist as cdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    cdist.init("gloo", timeout_s=5)
+    if rank == 1:  # this rank dies before the exchange (no destroy: it just vanishes)
+        os._exit(0)
+    rec = torch.zeros((10, 2), dtype=torch.int64)
+    t0 = time.time()
+    try:
+        cdist.allgather_cands(rec)
+        out[rank] = ("no error", time.time() - t0)
+    except Exception as e:  # noqa: BLE001 -- any failure is the point
+        out[rank] = (type(e).__name__, time.time() - t0)
+
+
+def test_dead_rank_fails_fast():
+    """SURVEY.md section 5 fail-fast: with ce_amd.dist.init's timeout a survivor's
+    collective raises instead of hanging on a rank that died (torch's default
+    would wait 10 minutes)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_dead_rank, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode is not None for p in procs), "a rank hung"
+    err, dt = out[0]
+    assert err != "no error" and dt < 60, (err, dt)
+
+
 def test_order_key_roundtrip():
     h = np.array([np.nan, 1.5, -0.0, 0.0, -np.inf, np.inf, 1e-300, -2.0])
     k = _order_key(h)

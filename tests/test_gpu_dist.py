@@ -155,4 +155,6 @@ def test_bench_world2_rehearsal():
     l1 = json.loads(one.stdout.strip().splitlines()[-1])
     l2 = json.loads(two.stdout.strip().splitlines()[-1])
     assert l2["n_gpus"] == 2 and l2["config"]["items_per_gpu"] == 1500001
+    assert l2["rehearsal"]["backend"] == "gloo" and l2["value"] is None  # never a valid-looking multi-GPU figure
+    assert "rehearsal" not in l1 and l1["value"] > 0
     assert l1["selected"] == l2["selected"] and len(l1["selected"]) == 10

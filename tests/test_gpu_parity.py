@@ -417,6 +417,31 @@ def test_small_pool_single_launch(ce, N):
         assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, q, "NMC")[1]), q
 
 
+def test_ticket_counters_return_to_zero(ce):
+    """The tiled small-pool kernels and the folded stage 2 draw arrival tickets
+    from the workspace header (include/ce.h: zero-filled before first use,
+    zero again after every call): after a run of every ticketed path, the
+    header is all zero and repeated calls keep selecting the same positions."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(4)
+    P = synth(rng, 3000, 4, 4, np.float32, quant=8)
+    Pm = dev(np.ascontiguousarray(np.transpose(P, (1, 0, 2))))
+    big = dev(synth(rng, 400_000, 16, 4))
+    hc = dev(np.round(rng.dirichlet(np.ones(4), 1500), 3))
+    offs = dev(np.array([0, 1000, 1000, 3000], np.int64))
+    exp = O.oracle_select_mc(P, 10, "NMC")[1]
+    for _ in range(3):
+        assert np.array_equal(idx_np(ce.ops.select_mc(Pm, 10, "MNC")[1]), exp)
+        ce.ops.select_mix(Pm, hc, 10)
+        ce.ops.select_batched(Pm, offs, 10)
+        ce.ops.select_mc(big, 10, "NMC")
+    torch.cuda.synchronize()
+    ws = ce.ops.WORKSPACE.get(torch.device("cuda", torch.cuda.current_device()), 0)
+    off = (-ws.data_ptr()) % 256
+    assert int(ws[off:off + 65536].count_nonzero()) == 0
+
+
 @pytest.mark.parametrize("world", [1, 2, 8])
 def test_record_exchange(ce, world):
     """The multi-GPU exchange on one device: each 'rank' scores its shard
@@ -436,6 +461,11 @@ def test_record_exchange(ce, world):
         plan = ce.ops.MCPlan(Pd[lo:hi], q, "NMC", base_idx=lo)
         plan.partial()
         recs.append(plan.finish_cands())
+        # the one-launch form (stage 2 folded into stage 1's last block) writes the same records
+        assert torch.equal(plan.step_cands(), recs[-1])
+        v1, i1 = plan.step()
+        v2, i2 = ce.ops.merge_cands(recs[-1], q)
+        assert torch.equal(i1, i2) and torch.equal(v1.view(torch.int64), v2.view(torch.int64))
     vals, idx = ce.ops.merge_cands(torch.cat(recs), q)
     vo, io = O.oracle_select_mc(P, q, "NMC")
     assert np.array_equal(idx_np(idx), io)
@@ -609,6 +639,40 @@ def test_session_rand_and_exhaustion(ce):
     for _ in range(25):
         sess.select(committee=P)
     assert sess.remaining == 0 and len(sess.select(committee=P)) == 0
+
+
+def test_session_rand_reference_stream(ce):
+    """SelectionSession("rand") draws what amg_test.py:486-489 draws, epoch
+    after epoch: the reference shuffles X_train.index.unique().tolist() (songs
+    in first-appearance order of the frame rows, NOT sorted) with the global
+    legacy RNG seeded by np.random.seed(1987) (:55), takes the first q, and
+    drops those songs' rows from X_train (:521-531)."""
+    import pandas as pd
+
+    rng = np.random.default_rng(5)
+    n_songs, q, epochs = 300, 10, 4
+    s_ids = rng.permutation(np.arange(1000, 1000 + 3 * n_songs, 3))       # song ids, not positions
+    frames = np.repeat(s_ids, rng.integers(1, 6, n_songs))                # frames per song
+    X_train = pd.DataFrame({"f": np.arange(len(frames))}, index=pd.Index(rng.permutation(frames), name="s_id"))
+    # the reference's loop
+    np.random.seed(1987)
+    exp, Xr = [], X_train
+    for _ in range(epochs):
+        pos_songs = Xr.index.unique().tolist()
+        np.random.shuffle(pos_songs)
+        q_songs = pos_songs[:q]
+        exp.append(q_songs)
+        Xr = Xr.drop(q_songs)
+    # the session: pool positions = sorted song ids (the committee's groupby order, :437)
+    uniq = np.unique(frames)
+    order = np.searchsorted(uniq, X_train.index.unique().to_numpy())  # first-appearance order as positions
+    np.random.seed(1987)
+    sess = ce.SelectionSession(q, "rand", len(uniq), rand_order=order)
+    for e in range(epochs):
+        got = uniq[sess.select()].tolist()
+        assert got == exp[e], (e, got, exp[e])
+    with pytest.raises(ValueError):
+        ce.SelectionSession(q, "rand", len(uniq), rand_order=order[:-1])
 
 
 @pytest.mark.parametrize("N,M,C,dt", [(2_000_000, 16, 4, np.float32), (1_000_000, 4, 4, np.float64),

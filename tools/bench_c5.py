@@ -92,9 +92,9 @@ def main():
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
     if world > 1:
-        import torch.distributed as dist
+        from ce_amd import dist as cdist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        cdist.init("nccl", device=torch.device("cuda", torch.cuda.current_device()))
     line = run(a.items, a.chunk, a.members, a.classes, a.q, rank=rank, world=world)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -4,6 +4,8 @@
 #   PHASE=check    pytest -m gpu, smoke(), bench.py (default line + A/B lines)
 #   PHASE=profile  rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
 #   PHASE=xgb      the same for the XGB member (tools/bench_configs.py --only 7)
+#   PHASE=small    kernel traces of the small-pool configs + PMC passes of one (tools/small_probe.py)
+#   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
 # Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -82,6 +84,26 @@ mpmc)  # PMC passes over the member kernels (tools/members_pmc.py): SQ occupancy
   step $? "mpmc ta"
   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS -d "$OUT/prof/mpmc_sq2" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" > "$OUT/mpmc_sq2.log" 2>&1
   step $? "mpmc sq2"
+  ;;
+small)  # single-block / small-pool configs: one kernel trace per config + PMC passes of configs[2] (dense)
+  cd /tmp
+  for c in ${CFGS:-c1 c2hc c2mix c3 c3r}; do
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof/${TAG}small_$c" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $c 200 > "$OUT/${TAG}small_$c.log" 2>&1
+    step $? "trace $TAG$c"
+  done
+  P=${PMCCFG:-c3}
+  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/${TAG}pmc_fetch" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_fetch.log" 2>&1
+  step $? "${TAG}pmc fetch"
+  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/${TAG}pmc_write" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_write.log" 2>&1
+  step $? "${TAG}pmc write"
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d "$OUT/prof/${TAG}pmc_sq" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_sq.log" 2>&1
+  step $? "${TAG}pmc sq"
+  timeout -s KILL 90 rocprofv3 --pmc TA_TA_BUSY_sum SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/${TAG}pmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_ta.log" 2>&1
+  step $? "${TAG}pmc ta"
+  ;;
+firstcall)  # first-call latency per library build (tools/first_call.py)
+  timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
+  step $? "first call"
   ;;
 *) echo "PHASE must be check, ab, profile, benchprof, configs, xgb or mpmc" >&2; exit 2 ;;
 esac
