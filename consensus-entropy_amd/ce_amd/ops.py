@@ -101,6 +101,20 @@ def log_f64(x):
     return y
 
 
+def row_div_f64(x, s):
+    """x / s as the engine divides each consensus row by its sum inside the
+    entropy (ce_row_div_f64: one reciprocal per row; verification against
+    IEEE division)."""
+    _on_gpu(x, "x")
+    x = x.contiguous().to(torch.float64)
+    s = s.contiguous().to(torch.float64)
+    if x.shape != s.shape:
+        raise ValueError("x and s must have one shape")
+    y = torch.empty_like(x)
+    call("ce_row_div_f64", _p(x), _p(s), x.numel(), _p(y), _stream(x.device))
+    return y
+
+
 def vote_table(votes, C=4):
     """amg_test.py:109-117 on int8 votes [N, A] (-1 = missing): (freq [N, C], ent [N])."""
     _on_gpu(votes, "votes")
@@ -156,6 +170,61 @@ def segment_mean(frames, offsets, perm=None, out=None):
     call("ce_segment_mean", _p(frames), _DT[frames.dtype], F, C, frames.stride(0), _p(perm), _p(offsets), N,
          _p(out), _DT[out.dtype], out.stride(0), _stream(frames.device))
     return out
+
+
+class _Member(ctypes.Structure):
+    """include/ce.h ce_member."""
+    _fields_ = [("p", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("song_level", ctypes.c_int32),
+                ("ld", ctypes.c_int64)]
+
+
+def select_frames(members, offsets, q, perm=None, base_idx=0, song_level=None):
+    """amg_test.py:426-445 from the members' FRAME-level outputs in one pass
+    (ce_select_frames): per member the groupby(['s_id'])
+    mean (:437), the member-sequential mean over the stack, the entropy and the
+    top-q over songs -- the [M, N, C] stack is never written.  ``members``:
+    device tensors [F, C] (frame rows, song n = rows perm[offsets[n]:
+    offsets[n+1]] or offsets[n]:offsets[n+1]) or [N, C] (song-level, e.g. the
+    CNN member); ``song_level`` overrides the shape rule per member.  q <= 64.
+    Returns (vals [q], idx [q]) over the N sorted songs."""
+    members = list(members)
+    if not members:
+        raise ValueError("committee has no members")
+    _on_gpu(offsets, "offsets")
+    offsets = offsets.to(torch.int64).contiguous()
+    N = offsets.numel() - 1
+    if N < 0:
+        raise ValueError("offsets must hold N + 1 entries")
+    if perm is not None:
+        _on_gpu(perm, "perm")
+        perm = perm.to(torch.int64).contiguous()
+    q = _check_q(q)
+    C = members[0].shape[1]
+    arr = (_Member * len(members))()
+    keep = []
+    F = perm.numel() if perm is not None else None
+    for m, t in enumerate(members):
+        _on_gpu(t, f"member {m}")
+        if t.dim() != 2 or t.shape[1] != C or t.dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"member {m} must be a float32/float64 [*, {C}] tensor")
+        if t.stride(1) != 1:
+            t = t.contiguous()
+        keep.append(t)
+        if song_level is not None:
+            sl = bool(song_level[m])
+        elif t.shape[0] != N:
+            sl = False
+        else:  # N rows: song-level unless there are exactly N frames too
+            if F is None:
+                F = int(offsets[-1])
+            sl = F != N
+        arr[m] = _Member(t.data_ptr(), _DT[t.dtype], 1 if sl else 0, t.stride(0))
+    lib = _lib.load()
+    ws = WORKSPACE.get(offsets.device, lib.ce_select_frames_workspace_bytes(N, q))
+    vals, idx = _outs(q, offsets.device)
+    call("ce_select_frames", ctypes.cast(arr, ctypes.c_void_p), len(members), C, _p(offsets), _p(perm), N, q,
+         int(base_idx), _p(ws), ws.numel(), _p(vals), _p(idx), _stream(offsets.device))
+    return vals, idx
 
 
 def _f64_dev(t, device, what):

@@ -123,6 +123,31 @@ def committee_from_frames(members, s_id, device=None):
     return stack, uniq
 
 
+def select_from_frames(members, s_id, q, device=None):
+    """amg_test.py:426-447 in ONE kernel from the members' frame-level outputs
+    (ops.select_frames): `members` in mod_list order, each a
+    frame-level predict_proba [F, C] (rows in X_train order, song ids `s_id`)
+    or a song-level [N, C] member (the CNN, :430-433); the [M, N, C] stack is
+    never built.  Returns (q_ind positions over the sorted songs, the sorted
+    song ids) -- q_songs = ids[q_ind] as :447 maps them."""
+    dev = _device(device)
+    uniq, offsets, perm = song_groups(s_id)
+    N, F = len(uniq), len(np.asarray(getattr(s_id, "values", s_id)))
+    ts, sl = [], []
+    for m, a in enumerate(members):
+        t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(getattr(a, "values", a)))
+        if t.dtype not in (torch.float32, torch.float64):
+            t = t.to(torch.float64)
+        if t.dim() != 2 or t.shape[0] not in (F, N):
+            raise ValueError(f"member {m} has shape {tuple(t.shape)}: neither {F} frames nor {N} songs")
+        ts.append(t.to(dev))
+        sl.append(not (t.shape[0] == F and (F != N or perm is not None)))  # committee_from_frames' rule
+    offs = torch.from_numpy(offsets).to(dev)
+    pd_ = torch.from_numpy(perm).to(dev) if perm is not None else None
+    _, idx = ops.select_frames(ts, offs, q, perm=pd_, song_level=sl)
+    return _positions(idx), uniq
+
+
 def _hc_tensor(hc, votes, C, dev):
     if hc is not None:
         arr = np.asarray(getattr(hc, "values", hc), dtype=np.float64) if not isinstance(hc, torch.Tensor) else hc

@@ -12,6 +12,14 @@ __global__ __launch_bounds__(kBS) void k_log(const double* __restrict__ x, int64
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) y[i] = dlog(x[i]);
 }
 
+// x[i] / s[i] through the entropy path's shared-reciprocal division
+// (RowDivisor, ce_device.hpp) -- verification against IEEE division.
+__global__ __launch_bounds__(kBS) void k_rowdiv(const double* __restrict__ x, const double* __restrict__ s, int64_t n,
+                                                double* __restrict__ y) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS)
+        y[i] = RowDivisor(s[i]).div(x[i]);
+}
+
 __global__ __launch_bounds__(kBS) void k_va(const double* __restrict__ va, int64_t N, int A,
                                             double* __restrict__ freq, double* __restrict__ ent) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
@@ -87,6 +95,14 @@ extern "C" int ce_log_f64(const double* x, int64_t n, double* y, ce_stream_t str
     const int grid = (int)std::min<int64_t>(cdiv(n, kBS), 8192);
     hipLaunchKernelGGL(k_log, dim3(grid), dim3(kBS), 0, (hipStream_t)stream, x, n, y);
     return check_launch("ce_log_f64");
+}
+
+extern "C" int ce_row_div_f64(const double* x, const double* s, int64_t n, double* y, ce_stream_t stream) {
+    if (n < 0 || (n > 0 && (!x || !s || !y))) return fail(CE_EINVAL, "bad division arguments");
+    if (n == 0) return CE_OK;
+    const int grid = (int)std::min<int64_t>(cdiv(n, kBS), 8192);
+    hipLaunchKernelGGL(k_rowdiv, dim3(grid), dim3(kBS), 0, (hipStream_t)stream, x, s, n, y);
+    return check_launch("ce_row_div_f64");
 }
 
 extern "C" int ce_log_f64_host(const double* x, int64_t n, double* y) {

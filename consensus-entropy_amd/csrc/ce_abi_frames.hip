@@ -1,0 +1,60 @@
+// ce_abi_frames.hip -- C-ABI (include/ce.h): frames -> committee entropy ->
+// top-q in one pass (k_frames_select, ce_frames.hpp).
+#include "ce_frames.hpp"
+#include "ce_host.hpp"
+
+using namespace ce;
+
+extern "C" size_t ce_select_frames_workspace_bytes(int64_t N, int32_t q) {
+    return lists_bytes(pool_blocks(N), q < 1 ? 1 : q);
+}
+
+extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, const int64_t* offsets,
+                                const int64_t* perm_or_null, int64_t N, int32_t q, int64_t base_idx, void* ws,
+                                size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    int rc = check_q(q);
+    if (rc) return rc;
+    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "frame selection needs q <= %d (got %d)", kStreamMaxQ, q);
+    if (!members || M < 1 || M > kMaxFrameMembers) return fail(CE_EINVAL, "need 1..%d members (got %d)", kMaxFrameMembers, M);
+    if (N < 0 || (N > 0 && !offsets) || !val_out || !idx_out) return fail(CE_EINVAL, "bad frame selection arguments");
+    if (C != 2 && C != 3 && C != 4 && C != 8) return fail(CE_EUNSUPPORTED, "frame selection: C=%d not in {2, 3, 4, 8}", C);
+    const int G = pool_blocks(N);
+    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    FrameArgs fa{};
+    for (int m = 0; m < M; ++m) {
+        const ce_member& x = members[m];
+        if (x.dtype != CE_F32 && x.dtype != CE_F64) return fail(CE_EUNSUPPORTED, "member %d: float32/float64 only", m);
+        if (!x.p && N > 0) return fail(CE_EINVAL, "member %d: null pointer", m);
+        if (x.ld < C) return fail(CE_EINVAL, "member %d: row stride %lld < C", m, (long long)x.ld);
+        const int eb = x.dtype == CE_F64 ? 8 : 4;
+        fa.mem[m] = FrameMember{x.p, x.ld, x.dtype == CE_F64 ? kF64 : kF32, x.song_level ? 1 : 0,
+                                ((uintptr_t)x.p % 16 == 0 && (x.ld * eb) % 16 == 0) ? 1 : 0, 0};
+    }
+    fa.M = M;
+    fa.off = offsets;
+    fa.perm = perm_or_null;
+    fa.N = N;
+    fa.dM = (double)M;
+    fa.invM = 1.0 / (double)M;
+    fa.pow2 = (M & (M - 1)) == 0;
+    fa.base_idx = base_idx;
+    fa.nlists = G;
+    hipStream_t st = (hipStream_t)stream;
+    WsLists w = carve(ws, G, q);
+    fa.ctr = w.ctr;
+    fa.oval = val_out;
+    fa.oidx = idx_out;
+    fa.ocand = nullptr;
+    auto go = [&](auto kern) {
+        const int grid = resident_grid(kern, 0, G);
+        fa.per_wave = (cdiv(N, (int64_t)grid * 4) + 63) / 64 * 64;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, fa, q, w.c);
+    };
+    switch (C) {
+        case 2: go(k_frames_select<2>); break;
+        case 3: go(k_frames_select<3>); break;
+        case 4: go(k_frames_select<4>); break;
+        default: go(k_frames_select<8>); break;
+    }
+    return check_launch("ce_select_frames");
+}

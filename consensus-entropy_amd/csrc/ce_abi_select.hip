@@ -78,7 +78,7 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
     }
     // large pools: the streaming stage 1 with stage 2 folded into its last block
     const int G = pool_blocks(N);
-    const int sr = launch_stream_fold(a, G, q, base_idx, carve(ws, G, q), st, excl, FoldOut{val_out, idx_out, nullptr});
+    const int sr = launch_stream_fold(a, G, q, base_idx, carve(ws, G, q), st, excl, FoldOut{val_out, idx_out, nullptr, nullptr});
     if (sr == 2) return check_launch("ce_select_mc");
     if (sr == 1) {
         finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
@@ -110,7 +110,7 @@ extern "C" int ce_select_mc_cands(const void* p, ce_dtype dt, int64_t N, int32_t
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, G, q);
     Cand* oc = reinterpret_cast<Cand*>(out);
-    const int sr = N > 0 ? launch_stream_fold(a, G, q, base_idx, w, st, nullptr, FoldOut{nullptr, nullptr, oc}) : 0;
+    const int sr = N > 0 ? launch_stream_fold(a, G, q, base_idx, w, st, nullptr, FoldOut{nullptr, nullptr, oc, nullptr}) : 0;
     if (sr == 2) return check_launch("ce_select_mc_cands");
     if (sr == 0) {  // no streaming kernel (or an empty pool): the block-synchronous stage 1
         Seg sg{nullptr, N, G, base_idx};
@@ -199,10 +199,25 @@ extern "C" int ce_select_mc_chunk(const void* p, ce_dtype dt, int64_t N, int32_t
     const int G = pool_blocks(N);
     if (!ws || ws_bytes < lists_bytes((int64_t)G + 1, q)) return fail(CE_EWORKSPACE, "workspace too small");
     WsLists w = carve(ws, (int64_t)G + 1, q);
+    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
+    {
+        const int rc0 = check_comm(a);
+        if (rc0) return rc0;
+    }
+    // one launch per chunk: the streaming stage 1 whose last block merges the
+    // grid's lists AND the running list back into `running`
+    const int sr = launch_stream_fold(a, G, q, base_idx, w, st, nullptr, FoldOut{nullptr, nullptr, run, first ? nullptr : run});
+    if (sr == 2) return check_launch("ce_select_mc_chunk");
+    if (sr == 1) {  // streamed without the fold: the lists are in the workspace
+        if (!first && hipMemcpyAsync(w.c + (int64_t)G * q, run, (size_t)q * sizeof(Cand), hipMemcpyDeviceToDevice,
+                                     st) != hipSuccess)
+            return fail(CE_ELAUNCH, "running-list copy failed");
+        launch_finish_lists(w.c, 1, G + (first ? 0 : 1), q, nullptr, nullptr, st, run);
+        return check_launch("ce_select_mc_chunk");
+    }
     if (!first && hipMemcpyAsync(w.c + (int64_t)G * q, run, (size_t)q * sizeof(Cand), hipMemcpyDeviceToDevice, st) !=
                       hipSuccess)
         return fail(CE_ELAUNCH, "running-list copy failed");
-    CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
     int Gs = 0;
     bool fin = false;
     rc = mc_partial(a, q, base_idx, ws, ws_bytes, nullptr, nullptr, false, &Gs, &fin, st);

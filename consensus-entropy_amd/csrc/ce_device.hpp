@@ -95,13 +95,54 @@ __device__ __forceinline__ double row_sum(const double (&a)[C]) {
     return 0.0 + pairwise<0, C, C>(a);
 }
 
+// ---------------------------------------------------------------------------
+// x / s for many x and one s, bit-identical to separate IEEE divisions.
+// gfx950's f64 division (LLVM's lowering; see DESIGN.md "Numerics") is
+//   d = v_div_scale(s), n = v_div_scale(x); r = v_rcp_f64(d), two Newton steps
+//   r = fma(r, fma(-d, r, 1), r); q = n * r; rem = fma(-d, q, n);
+//   v_div_fmas(rem, r, q) = fma(rem, r, q) (+ rescale); v_div_fixup (specials)
+// When neither operand needs scaling -- both in [2^-300, 2^300), or x == 0 --
+// the scale steps return their input, v_div_fmas is a plain fma and
+// v_div_fixup returns its input, so r depends on s alone: the row's C
+// quotients cost 5 + 3C instructions instead of ~11C.  Anything else (zero,
+// tiny, huge, inf, NaN) takes the ordinary division.  Opt-in (-DCE_FASTDIV,
+// the A/B build `make fastdiv`): the device test found pairs outside the
+// probability regime where it differs from IEEE division.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool div_plain_range(double x) {  // exponent field in [1023-300, 1023+300)
+    return ((((uint32_t)(dbits(x) >> 32)) >> 20) & 0x7ffu) - 723u < 600u;
+}
+struct RowDivisor {
+    double s, r;
+    bool fast;
+    __device__ __forceinline__ explicit RowDivisor(double s_) : s(s_), r(0.0), fast(div_plain_range(s_)) {
+#ifdef CE_FASTDIV
+        if (fast) {
+            double r0 = __builtin_amdgcn_rcp(s);
+            r0 = __builtin_fma(r0, __builtin_fma(-s, r0, 1.0), r0);
+            r = __builtin_fma(r0, __builtin_fma(-s, r0, 1.0), r0);
+        }
+#endif
+    }
+    __device__ __forceinline__ double div(double x) const {
+#ifdef CE_FASTDIV
+        if (fast && (x == 0.0 || div_plain_range(x))) {
+            const double q = x * r;
+            return __builtin_fma(__builtin_fma(-s, q, x), r, q);
+        }
+#endif
+        return x / s;
+    }
+};
+
 // scipy.stats.entropy of one row held in registers (mean: consensus row).
 template <int C>
 __device__ __forceinline__ double entropy_row(const double (&mean)[C]) {
     const double s = row_sum<C>(mean);
+    const RowDivisor d(s);
     double e[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) e[c] = entr(1.0 * mean[c] / s);
+    for (int c = 0; c < C; ++c) e[c] = entr(d.div(1.0 * mean[c]));
     return row_sum<C>(e);
 }
 

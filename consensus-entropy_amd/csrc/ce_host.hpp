@@ -241,6 +241,7 @@ static inline StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx)
     s.oval = nullptr;
     s.oidx = nullptr;
     s.ocand = nullptr;
+    s.extra = nullptr;
     return s;
 }
 
@@ -274,6 +275,7 @@ struct FoldOut {
     double* oval;
     int64_t* oidx;
     Cand* ocand;
+    const Cand* extra;  // one more list to merge (a chunked job's running list), or nullptr
 };
 CE_HIDDEN int launch_stream_fold(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                                  const uint32_t* excl, FoldOut out);

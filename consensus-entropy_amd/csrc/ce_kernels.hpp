@@ -376,7 +376,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
         }
     }
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
-    if (sa.ctr) fold_merge<4>(sa, q, wc, sm);
+    if (sa.ctr) fold_merge<4>(sa.ctr, sa.oval, sa.oidx, sa.ocand, q, wc, sm, sa.extra);
 }
 
 template <int DT, int NPL, bool VEC>

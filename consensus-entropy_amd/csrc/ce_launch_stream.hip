@@ -59,6 +59,7 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
         sa.oval = fold->oval;
         sa.oidx = fold->oidx;
         sa.ocand = fold->ocand;
+        sa.extra = fold->extra;
     }
     const int folded = fold ? 2 : 1;
     const int eb = elem_bytes(a.dt);

@@ -372,6 +372,7 @@ struct StreamArgs {
     double* oval;
     int64_t* oidx;
     Cand* ocand;
+    const Cand* extra;  // one more list merged by the fold (chunked jobs: the running list), or nullptr
 };
 
 // Merge the block's WAVES wave lists (registers, best-first) into the
@@ -448,8 +449,21 @@ struct ListSrc {
 // enter the register lists.  One round of head loads (nl / (64 W) per lane)
 // plus ~q list loads per block instead of all nl * q candidates.
 // bk / bi: W-entry LDS scratch; L: the block-merge scratch.
-template <int W, bool FROM_VALS>
-__device__ inline void merge_lists_block(ListSrc<FROM_VALS> src, int64_t seg0, int nl, int q, WaveListsT<W>& L,
+// The grid's lists followed by one extra list elsewhere (a chunked job's
+// running top-q): list g < na at a[g*q..], list na at extra[0..q).
+struct FoldSrc {
+    const Cand* a;
+    int64_t na_q;  // na * q
+    const Cand* extra;
+    __device__ __forceinline__ void get(int64_t j, uint64_t& k, int64_t& i) const {
+        const Cand x = j < na_q ? a[j] : extra[j - na_q];
+        k = x.key;
+        i = x.idx;
+    }
+};
+
+template <int W, class Src>
+__device__ inline void merge_lists_block(Src src, int64_t seg0, int nl, int q, WaveListsT<W>& L,
                                          uint64_t* bk, int64_t* bi, double* oval, int64_t* oidx, Cand* ocand) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     RegTopQ hq;
@@ -500,20 +514,23 @@ __device__ inline void merge_lists_block(ListSrc<FROM_VALS> src, int64_t seg0, i
 // takes a ticket; the block that draws gridDim.x - 1 fences (acquire), resets
 // the counter and merges the grid's lists into the final output / records.
 template <int W>
-__device__ inline void fold_merge(const StreamArgs& a, int q, const Cand* wc0, WaveListsT<W>& L) {
+__device__ inline void fold_merge(uint32_t* ctr, double* oval, int64_t* oidx, Cand* ocand, int q, const Cand* wc0,
+                                  WaveListsT<W>& L, const Cand* extra = nullptr) {
     __shared__ int ticket;
     __shared__ uint64_t bk[W];
     __shared__ int64_t bi[W];
     __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) ticket = (int)atomicAdd(a.ctr, 1u);
+    if (threadIdx.x == 0) ticket = (int)atomicAdd(ctr, 1u);
     __syncthreads();
     CE_DASSERT(ticket >= 0 && ticket < (int)gridDim.x);
     if (ticket != (int)gridDim.x - 1) return;  // block-uniform
     __threadfence();
-    if (threadIdx.x == 0) atomicExch(a.ctr, 0u);
-    merge_lists_block<W, false>(ListSrc<false>{wc0, nullptr, nullptr}, 0, gridDim.x, q, L, bk, bi, a.oval, a.oidx,
-                                a.ocand);
+    if (threadIdx.x == 0) atomicExch(ctr, 0u);
+    // extra (a chunked job's running list) may be ocand itself: every input is in
+    // registers before block_merge_write stores the result
+    merge_lists_block<W>(FoldSrc{wc0, (int64_t)gridDim.x * q, extra}, 0, (int)gridDim.x + (extra ? 1 : 0), q, L, bk,
+                         bi, oval, oidx, ocand);
 }
 
 // Item-major, dense rows of 16*S bytes, LDS-DMA staged (AUX: DMA cache policy);
@@ -559,7 +576,7 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
         tq.offer(order_key(h), i + a.base_idx, ok);
     }
     block_merge_write<4>(tq, sm.lists, q, wc + (int64_t)blockIdx.x * q, a.nlists);
-    if (a.ctr) fold_merge<4>(a, q, wc, sm.lists);
+    if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm.lists, a.extra);
 }
 
 // Any strides (vector loads when aligned): member-major [M, N, C] streams
@@ -603,7 +620,7 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     tq.init(q);
     stream_direct_range<Src, IPL, UNR>(src, lo, hi, a.base_idx, q, tq, a.excl);
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists);
-    if (a.ctr) fold_merge<4>(a, q, wc, sm);
+    if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm, a.extra);
 }
 
 // Batched pools (amg_test.py:345's per-user loop in one launch): user u owns

@@ -169,10 +169,11 @@ __device__ inline double wave_item_entropy(const void* p, int64_t off, int M, in
     __builtin_amdgcn_wave_barrier();
     const double s = wave_row_sum(row, pl, scratch);
     __builtin_amdgcn_wave_barrier();
+    const RowDivisor d(s);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int c = lane + 64 * k;
-        if (c < C) row[rp(c)] = entr(1.0 * acc[k] / s);
+        if (c < C) row[rp(c)] = entr(d.div(1.0 * acc[k]));
     }
     __builtin_amdgcn_wave_barrier();
     const double h = wave_row_sum(row, pl, scratch);
@@ -234,12 +235,13 @@ __device__ __forceinline__ double wave_entropy_from_sums(double* acc, int K, dou
     __builtin_amdgcn_wave_barrier();
     const double s = wave_row_sum(row, pl, scratch);
     __builtin_amdgcn_wave_barrier();
+    const RowDivisor d(s);  // the row's quotients share the divisor's reciprocal (ce_device.hpp)
 #pragma unroll
     for (int kk = 0; kk < KCH; ++kk) {
         const int ch = lane + 64 * kk;
 #pragma unroll
         for (int e = 0; e < CPC; ++e)
-            if (ch < K) row[rp(ch * CPC + e)] = entr(1.0 * acc[kk * CPC + e] / s);
+            if (ch < K) row[rp(ch * CPC + e)] = entr(d.div(1.0 * acc[kk * CPC + e]));
     }
     __builtin_amdgcn_wave_barrier();
     const double h = wave_row_sum(row, pl, scratch);

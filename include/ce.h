@@ -110,6 +110,35 @@ int ce_segment_mean(const void *frames, ce_dtype dt, int64_t F, int32_t C, int64
                     ce_dtype out_dt, int64_t ld_out, ce_stream_t stream);
 
 /*
+ * Frames -> committee entropy -> top-q in ONE pass --
+ * replaces amg_test.py:426-445 from the members' FRAME-level outputs on: per
+ * member, pd.DataFrame(y_probs, index=X_train.index).groupby(['s_id']).mean()
+ * (:437; pandas 1.1.5 group_mean, as ce_segment_mean), then
+ * np.mean(np.array(pred_prob), 0), scipy.stats.entropy and argsort[::-1][:q]
+ * (:441-445) -- without materialising the [M, N, C] stack.
+ * members: HOST array of M (<= 32) descriptors, in mod_list order; a member is
+ * frame-level (rows of X_train: song n owns rows perm[offsets[n]] ..
+ * perm[offsets[n+1]-1], perm_or_null == NULL: offsets[n] .. offsets[n+1]-1)
+ * or song-level (song_level != 0: row n, e.g. the CNN member, :430-433).
+ * Every member is f32/f64 [*, C] with row stride ld; a float32 member's song
+ * means are rounded to float32 (the groupby result keeps the dtype) and the
+ * stack is accumulated in f64 (north star: fp32 load, fp64 accumulate).
+ * C in {2, 3, 4, 8}; q <= 64; output as ce_select_mc (positions base_idx + n
+ * of the sorted songs).
+ */
+typedef struct {
+    const void *p;
+    int32_t dtype;      /* CE_F32 | CE_F64 */
+    int32_t song_level; /* 0: frame rows, 1: one row per song */
+    int64_t ld;         /* row stride, elements */
+} ce_member;
+
+size_t ce_select_frames_workspace_bytes(int64_t N, int32_t q);
+int ce_select_frames(const ce_member *members, int32_t M, int32_t C, const int64_t *offsets,
+                     const int64_t *perm_or_null, int64_t N, int32_t q, int64_t base_idx, void *ws,
+                     size_t ws_bytes, double *val_out, int64_t *idx_out, ce_stream_t stream);
+
+/*
  * Committee member inference on the device -- the
  * predict_proba of the reference's linear members (amg_test.py:435, :467;
  * deam_classifier.py:211-218) over frames X [F, D] f64 (row stride ld),
@@ -165,6 +194,10 @@ int ce_xgb_expf(const float *x, int64_t n, float *y, ce_stream_t stream);
  *                    synchronous, no GPU needed)
  */
 int ce_log_f64(const double *x, int64_t n, double *y, ce_stream_t stream);
+/* y[i] = x[i] / s[i] as every entropy divides its row by the row sum (one
+ * reciprocal per row, ce_device.hpp RowDivisor) -- verification against IEEE
+ * division (device memory, stream-ordered). */
+int ce_row_div_f64(const double *x, const double *s, int64_t n, double *y, ce_stream_t stream);
 int ce_log_f64_host(const double *x, int64_t n, double *y);
 
 /*

@@ -265,6 +265,42 @@ def test_device_log_bit_exact(ce):
     assert bad == 0
 
 
+def test_row_division_bit_exact(ce):
+    """The entropy's row division (one shared reciprocal per row, exact by
+    construction -- DESIGN.md 'Numerics') equals IEEE x / s on 6e7 pairs:
+    probabilities over row sums, random exponents across and beyond the fast
+    range [2^-300, 2^300), its boundaries +- a few ulps, zeros, signed zeros,
+    negatives, subnormals, inf and NaN."""
+    rng = np.random.default_rng(77)
+    n = 20_000_000
+    parts = []
+    s = rng.uniform(0.5, 2.0, n)
+    parts.append((rng.random(n) * s, s))
+    e1, e2 = rng.integers(-1100, 1024, n), rng.integers(-1100, 1024, n)
+    parts.append((np.ldexp(rng.uniform(-1, 1, n), e1), np.ldexp(rng.uniform(-1, 1, n), e2)))
+    edges = np.array([2.0 ** -300, 2.0 ** 300, 2.0 ** -301, 2.0 ** 299, 5e-324, 2.2250738585072014e-308,
+                      1.7976931348623157e308, np.inf, -np.inf, np.nan, 0.0, -0.0, 1.0, -1.0])
+    edges = np.concatenate([edges, np.nextafter(edges[:4], np.inf), np.nextafter(edges[:4], -np.inf)])
+    xs, ss = np.meshgrid(edges, edges)
+    parts.append((xs.ravel(), ss.ravel()))
+    k = rng.integers(-320, 320, n)
+    parts.append((np.ldexp(rng.random(n), k), np.ldexp(rng.uniform(0.5, 1.0, n), -k // 2)))
+    bad = 0
+    for p, (x, sv) in enumerate(parts):
+        got = ce.ops.row_div_f64(dev(x), dev(sv)).cpu().numpy()
+        with np.errstate(all="ignore"):
+            exp = x / sv
+        same = (got.view(np.int64) == exp.view(np.int64)) | (np.isnan(got) & np.isnan(exp))
+        nb = int((~same).sum())
+        if nb:
+            w = np.flatnonzero(~same)[:12]
+            print(f"part {p}: {nb} mismatches, e.g.")
+            for i in w:
+                print(f"  x={x[i].hex()} s={sv[i].hex()} got={got[i].hex()} ieee={exp[i].hex()}")
+        bad += nb
+    assert bad == 0
+
+
 def _bf16_bits(P32):
     """float32 -> bf16 bit patterns (round to nearest even), as uint16."""
     u = P32.astype(np.float32).view(np.uint32).astype(np.uint64)
@@ -525,6 +561,46 @@ def test_frames_to_selection(ce):
     assert np.array_equal(stack.cpu().numpy(), P)
     _, idx = ce.ops.select_mc(stack, 10, "MNC")
     assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, 10, "MNC")[1])
+
+
+@pytest.mark.parametrize("grouped", [False, True])
+def test_frames_fused_selection(ce, grouped):
+    """SURVEY.md §8(f)1 in one kernel (ce_select_frames): frame-level members
+    (f64, f64, f32 -- GNB/SGD/XGB over X_train rows, NaN cells included), a
+    song-level f32 member (the CNN), shuffled or grouped frame order, a song
+    whose frames are all NaN in one member (its mean is NaN: the song's
+    entropy is NaN and it ranks first) -- equal to the restated groupby mean
+    (amg_test.py:437) stacked like np.array(pred_prob) (:441) and selected by
+    the oracle (:443-445), for q = 1, 10, 64."""
+    from oracle import ce_oracle as O
+    from oracle.ce_oracle import ref_group_mean
+
+    rng = np.random.default_rng(21 + grouped)
+    F, C = 60_000, 4
+    s_id = rng.integers(0, 2500, F) * 7 + 3
+    if grouped:
+        s_id = np.sort(s_id)
+    frame_members = []
+    for dt in (np.float64, np.float64, np.float32):
+        e = -np.log(rng.random((F, C)))
+        fm = (e / e.sum(-1, keepdims=True))
+        fm[rng.random((F, C)) < 0.01] = np.nan
+        frame_members.append(fm.astype(dt))
+    nan_song = s_id[5]
+    frame_members[1][s_id == nan_song] = np.nan
+    n_songs = len(np.unique(s_id))
+    cnn = rng.random((n_songs, C)).astype(np.float32)
+    members = frame_members + [cnn]
+    pred_prob = [ref_group_mean(m, s_id)[0] for m in frame_members] + [cnn]
+    P = np.array(pred_prob)
+    for q in (1, 10, 64):
+        got, uniq = ce.select_from_frames(members, s_id, q)
+        exp = O.oracle_select_mc(P, q, "MNC")[1]
+        assert np.array_equal(got, exp), (q, got[:5], exp[:5])
+    assert uniq[got[0]] == nan_song  # NaN entropy first
+    # the same through the two-step path (segment means -> stack -> select_mc)
+    stack, _ = ce.committee_from_frames(members, s_id)
+    assert np.array_equal(idx_np(ce.ops.select_mc(stack, 10, "MNC")[1]), O.oracle_select_mc(P, 10, "MNC")[1])
 
 
 def _shrinking_reference(mode, epochs, q, committees, hc):

@@ -56,6 +56,35 @@ def test_new_entry_points_validate_without_gpu():
     rc = lib.ce_sgd_predict_proba(p, 10, 260, 260, p, p, 3, 4, p, 4, None)
     assert rc == _lib.CE_EINVAL
     assert lib.ce_mark_selected(None, 10, p, 1, 0, None) == _lib.CE_EINVAL
+    # one-launch records: q > 64 unsupported, misaligned output rejected
+    assert lib.ce_select_mc_cands(p, 0, 100, 4, 4, 16, 4, 1, 65, 0, p, 1 << 20, p, None) == _lib.CE_EUNSUPPORTED
+    assert lib.ce_select_mc_cands(p, 0, 100, 4, 4, 16, 4, 1, 10, 0, p, 1 << 20, ctypes.c_void_p(24),
+                                  None) == _lib.CE_EINVAL
+    assert lib.ce_row_div_f64(p, p, -1, p, None) == _lib.CE_EINVAL
+
+
+def test_frames_entry_validates_without_gpu():
+    """ce_select_frames: member count, class count, dtype, q and workspace are
+    checked on the host before anything launches."""
+    from ce_amd import _lib
+    from ce_amd.ops import _Member
+
+    lib = _lib.load()
+    p = ctypes.c_void_p(256)
+    ws = lib.ce_select_frames_workspace_bytes(1000, 10)
+    assert ws >= 65536 + 16 * 10
+    mem = (_Member * 2)(_Member(256, 0, 0, 4), _Member(256, 1, 1, 4))
+    args = lambda M, C, q, wsb, m=mem: (ctypes.cast(m, ctypes.c_void_p), M, C, p, None, 1000, q, 0, p, wsb, p, p,
+                                        None)
+    assert lib.ce_select_frames(*args(0, 4, 10, ws)) == _lib.CE_EINVAL          # no member
+    assert lib.ce_select_frames(*args(33, 4, 10, ws)) == _lib.CE_EINVAL         # too many
+    assert lib.ce_select_frames(*args(2, 5, 10, ws)) == _lib.CE_EUNSUPPORTED    # C = 5
+    assert lib.ce_select_frames(*args(2, 4, 65, ws)) == _lib.CE_EUNSUPPORTED    # q > 64
+    assert lib.ce_select_frames(*args(2, 4, 10, 64)) == _lib.CE_EWORKSPACE      # workspace
+    bad = (_Member * 1)(_Member(256, 2, 0, 4))                                   # bf16 member
+    assert lib.ce_select_frames(*args(1, 4, 10, ws, bad)) == _lib.CE_EUNSUPPORTED
+    short = (_Member * 1)(_Member(256, 0, 0, 3))                                 # row stride < C
+    assert lib.ce_select_frames(*args(1, 4, 10, ws, short)) == _lib.CE_EINVAL
 
 
 def test_python_guards_without_gpu():

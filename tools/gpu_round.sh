@@ -6,6 +6,7 @@
 #   PHASE=xgb      the same for the XGB member (tools/bench_configs.py --only 7)
 #   PHASE=small    kernel traces of the small-pool configs + PMC passes of one (tools/small_probe.py)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
+#   PHASE=debug    pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 # Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -100,6 +101,10 @@ small)  # single-block / small-pool configs: one kernel trace per config + PMC p
   step $? "${TAG}pmc sq"
   timeout -s KILL 90 rocprofv3 --pmc TA_TA_BUSY_sum SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/${TAG}pmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_ta.log" 2>&1
   step $? "${TAG}pmc ta"
+  ;;
+debug)  # the whole GPU suite once on the debug build (device bounds checks: make -C consensus-entropy_amd debug)
+  CE_AMD_LIB=$ROOT/tools/_diag/libce_amd_debug.so timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest_gpu_debug.log" 2>&1
+  step $? "pytest debug build"
   ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
