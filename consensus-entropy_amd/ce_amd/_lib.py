@@ -93,7 +93,12 @@ def load():
                     "`make -C consensus-entropy_amd`). There is no CPU fallback.")
             lib = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
-                f = getattr(lib, name)
+                try:
+                    f = getattr(lib, name)
+                except AttributeError:
+                    if os.environ.get("CE_AMD_LIB"):  # an older A/B build: bind what it exports
+                        continue
+                    raise
                 f.restype = res
                 f.argtypes = args
             _lib = lib

@@ -105,9 +105,10 @@ __device__ __forceinline__ double row_sum(const double (&a)[C]) {
 // the scale steps return their input, v_div_fmas is a plain fma and
 // v_div_fixup returns its input, so r depends on s alone: the row's C
 // quotients cost 5 + 3C instructions instead of ~11C.  Anything else (zero,
-// tiny, huge, inf, NaN) takes the ordinary division.  Opt-in (-DCE_FASTDIV,
-// the A/B build `make fastdiv`): the device test found pairs outside the
-// probability regime where it differs from IEEE division.
+// tiny, huge, inf, NaN) takes the ordinary division; a zero numerator returns
+// x * r, whose sign is IEEE's (the first device test caught -0 / s giving +0
+// through the correction step).  Opt-in (-DCE_FASTDIV, the A/B build `make
+// fastdiv`) until the device test holds it bit-exact.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool div_plain_range(double x) {  // exponent field in [1023-300, 1023+300)
     return ((((uint32_t)(dbits(x) >> 32)) >> 20) & 0x7ffu) - 723u < 600u;
@@ -126,9 +127,11 @@ struct RowDivisor {
     }
     __device__ __forceinline__ double div(double x) const {
 #ifdef CE_FASTDIV
-        if (fast && (x == 0.0 || div_plain_range(x))) {
-            const double q = x * r;
-            return __builtin_fma(__builtin_fma(-s, q, x), r, q);
+        const bool zero = x == 0.0;
+        if (fast && (zero || div_plain_range(x))) {
+            const double q = x * r;  // a zero numerator: +-0 with IEEE's sign (the correction would give +0)
+            const double res = __builtin_fma(__builtin_fma(-s, q, x), r, q);
+            return zero ? q : res;
         }
 #endif
         return x / s;

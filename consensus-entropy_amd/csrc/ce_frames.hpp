@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void k_frames_select(FrameArgs a, int q, Cand*
         const double h = entropy_row<C>(mean);
         tq.offer(order_key(h), n + a.base_idx, live);
     }
-    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists);
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists, nullptr, nullptr, 4, a.ctr != nullptr);
     if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm);
 }
 

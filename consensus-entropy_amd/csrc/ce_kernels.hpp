@@ -302,8 +302,16 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 // has 2 x UNR x KCH 16-B loads per lane outstanding.  Items per wave are not
 // rounded to 64 (a wide item is tens of KB): every wave of the resident grid
 // gets work.
+// A/B builds (make wide_ab): -DCE_WIDE2_WPE4 caps the wide stream at 128
+// VGPRs (4 waves per SIMD); -DCE_WIDE_ENTR_LDS feeds its entr pass from the
+// LDS row (wave_entropy_from_sums_lds: fewer live registers in that phase).
+#ifdef CE_WIDE2_WPE4
+#define CE_WIDE2_WPE __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define CE_WIDE2_WPE
+#endif
 template <int DT, int KCH, int UNR, int NB = 2>
-__global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
+__global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     CE_DASSERT((int)gridDim.x <= sa.nlists && q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
@@ -349,7 +357,11 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
         X.add(acc);
         if (++cb == NBM) {  // item ci complete
             cb = 0;
+#ifdef CE_WIDE_ENTR_LDS
+            const double h = wave_entropy_from_sums_lds<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
+#else
             const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
+#endif
 #pragma unroll
             for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
             const int j = (int)((ci - lo) & 63);
@@ -375,7 +387,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
             if (ci >= hi) break;
         }
     }
-    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists);
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists, nullptr, nullptr, 4, sa.ctr != nullptr);
     if (sa.ctr) fold_merge<4>(sa.ctr, sa.oval, sa.oidx, sa.ocand, q, wc, sm, sa.extra);
 }
 

@@ -6,49 +6,55 @@
 
 using namespace ce;
 
-// Tiled small pools (k_select_tiles, ce_small.hpp).  IPT items per thread
-// (2 for C = 8 rows), so a tile holds up to kTileBS * IPT items; UNR member
-// loads per item in flight (f64 / C = 8 rows are twice as wide: 2).
+// Small pools (k_select_tiles, ce_small.hpp).  IPT items per thread (2 for
+// C = 8 rows), so a tile holds up to BS * IPT items; UNR member loads per item
+// in flight (f64 / C = 8 rows, and 16-wave blocks, take 2).
 template <class Src>
 constexpr int small_ipt() { return Src::kC > 4 ? 2 : 4; }
-template <class Src>
-constexpr int small_unr() { return (Src::kDT == kF64 || Src::kC > 4) ? 2 : 4; }
+template <class Src, int BS>
+constexpr int small_unr() { return (Src::kDT == kF64 || Src::kC > 4 || BS > 512) ? 2 : 4; }
 
-// Tile-size targets (items per tile).  A/B knobs: CE_AMD_TILE_POOL (one pool,
+// Default: ONE block per problem (S = 1: the whole pool / user / mix selected
+// by one block, no hand-off).  Measured on MI355X (profiles/r03_small.json):
+// splitting a problem over S > 1 tiles with the arrival-ticket merge was
+// slower at the reference's sizes -- the hand-off (write-through lists, one
+// agent-scope atomic, sc1 reads by the last tile) costs more than spreading
+// 1608 items over more CUs saves (C1 9.4 -> 11.1-13.0 us, C3 15.7 -> 19.0 us).
+// A/B knobs, items per tile (> 0 enables tiling): CE_AMD_TILE_POOL (one pool,
 // the hc table), CE_AMD_TILE_USER (batched users), CE_AMD_TILE_MIX (each mix
 // segment).
-static int64_t tile_target(const char* env, int64_t dflt) {
+static int64_t tile_target(const char* env) {
     const char* e = getenv(env);
     const long v = e ? atol(e) : 0;
-    return v > 0 ? (int64_t)v : dflt;
+    return v > 0 ? (int64_t)v : 0;
 }
 static int64_t target_pool() {
-    static const int64_t v = tile_target("CE_AMD_TILE_POOL", 256);
+    static const int64_t v = tile_target("CE_AMD_TILE_POOL");
     return v;
 }
 static int64_t target_user() {
-    static const int64_t v = tile_target("CE_AMD_TILE_USER", 1024);
+    static const int64_t v = tile_target("CE_AMD_TILE_USER");
     return v;
 }
 static int64_t target_mix() {
-    static const int64_t v = tile_target("CE_AMD_TILE_MIX", 256);
+    static const int64_t v = tile_target("CE_AMD_TILE_MIX");
     return v;
 }
 
 // tiles for `len` items at <= `target` per tile, within the merge's capacity
 static int tiles_for(int64_t len, int64_t target, int q, int smax) {
+    if (target <= 0) return 1;
     int64_t s = cdiv(len < 1 ? 1 : len, target);
     const int64_t cap = std::min<int64_t>(smax, kTileMergeCap / q);
     if (s > cap) s = cap;
     return (int)(s < 1 ? 1 : s);
 }
 
-template <class SrcA, class SrcB, int IPTA, int IPTB>
+template <class SrcA, class SrcB, int IPTA, int IPTB, int BS>
 static void launch_tiles(const SrcA& a, const SrcB& b, const TileArgs& ta, int problems, int q, double* oval,
                          int64_t* oidx, const uint32_t* excl, hipStream_t st) {
-    hipLaunchKernelGGL((k_select_tiles<SrcA, SrcB, IPTA, IPTB, small_unr<SrcA>(), 1, kTileBS>),
-                       dim3((unsigned)(problems * (ta.SA + ta.SB))), dim3(kTileBS), 0, st, a, b, ta, q, oval, oidx,
-                       excl);
+    hipLaunchKernelGGL((k_select_tiles<SrcA, SrcB, IPTA, IPTB, small_unr<SrcA, BS>(), 1, BS>),
+                       dim3((unsigned)(problems * (ta.SA + ta.SB))), dim3(BS), 0, st, a, b, ta, q, oval, oidx, excl);
 }
 
 bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval, int64_t* oidx, const uint32_t* excl,
@@ -57,10 +63,20 @@ bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval,
     bool launched = false;
     const int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
+        constexpr int IPT = small_ipt<S>();
         const int SA = tiles_for(a.N, target_pool(), q, 16);
-        if (cdiv(a.N, SA) > (int64_t)kTileBS * small_ipt<S>()) return;  // tiles would be long: not this path
+        const int64_t per = cdiv(a.N, SA);
         const TileArgs ta{nullptr, a.N, 0, base_idx, SA, 0, w.c, w.ctr};
-        launch_tiles<S, S, small_ipt<S>(), 0>(src, src, ta, 1, q, oval, oidx, excl, st);
+        if (SA > 1) {
+            if (per > (int64_t)kTileBS * IPT) return;  // tiles would be long: not this path
+            launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, 1, q, oval, oidx, excl, st);
+        } else if (per <= 512 * IPT) {
+            launch_tiles<S, S, IPT, 0, 512>(src, src, ta, 1, q, oval, oidx, excl, st);
+        } else if (per <= 1024 * IPT) {
+            launch_tiles<S, S, IPT, 0, 1024>(src, src, ta, 1, q, oval, oidx, excl, st);
+        } else {
+            return;
+        }
         launched = true;
     });
     return rc == CE_OK && launched;
@@ -79,34 +95,46 @@ bool launch_small_users(const CommArgs& a, const int64_t* offsets, int U, int q,
     bool launched = false;
     const int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
+        constexpr int IPT = small_ipt<S>();
         // the average user must fit its tiles (a longer one streams inside its tile)
-        if (cdiv(cdiv(a.N, U), SA) > (int64_t)kTileBS * small_ipt<S>()) return;
+        const int64_t per = cdiv(cdiv(a.N, U), SA);
         const TileArgs ta{offsets, 0, 0, 0, SA, 0, w.c, w.ctr};
-        launch_tiles<S, S, small_ipt<S>(), 0>(src, src, ta, U, q, oval, oidx, nullptr, st);
+        if (SA > 1) {
+            if (per > (int64_t)kTileBS * IPT) return;
+            launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, U, q, oval, oidx, nullptr, st);
+        } else {  // one 512-thread block per user: 2 per CU, all 500 users of configs[2] resident
+            if (per > (int64_t)512 * IPT) return;
+            launch_tiles<S, S, IPT, 0, 512>(src, src, ta, U, q, oval, oidx, nullptr, st);
+        }
         launched = true;
     });
     return rc == CE_OK && launched;
 }
 
 // mix: committee items (segment A) then the hc table rows (segment B, a
-// 1-member f64 committee), 2 items per thread per segment
+// 1-member f64 committee), 2 items per thread per segment: one 1024-thread
+// block (S = 1, up to 2048 + 2048 rows) or 256-thread tiles
 bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, double* oval, int64_t* oidx, WsLists w,
                       hipStream_t st) {
     if (a.N < 1 || t.N < 1) return false;
+    const bool tiled = target_mix() > 0;
     const int SA = tiles_for(a.N, target_mix(), q, 8), SB = tiles_for(t.N, target_mix(), q, 8);
-    if (cdiv(a.N, SA) > 2 * kTileBS || cdiv(t.N, SB) > 2 * kTileBS || (SA + SB) * q > kTileMergeCap) return false;
-    const TileArgs ta{nullptr, a.N, t.N, 0, SA, SB, w.c, w.ctr};
+    const int BS = tiled ? kTileBS : 1024;
+    if (cdiv(a.N, SA) > 2 * BS || cdiv(t.N, SB) > 2 * BS || (SA + SB) * q > kTileMergeCap) return false;
+    const TileArgs ta{nullptr, a.N, t.N, 0, tiled ? SA : 1, tiled ? SB : 0, w.c, w.ctr};
     bool launched = false;
     const int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
         if constexpr (S::kC == 4 || S::kC == 8) {
             constexpr int CC = S::kC;
-            if (vec_ok(t, CC))
-                launch_tiles<S, CommitteeSrc<kF64, CC, true>, 2, 2>(src, make_src<kF64, CC, true>(t), ta, 1, q, oval,
-                                                                     oidx, nullptr, st);
-            else
-                launch_tiles<S, CommitteeSrc<kF64, CC, false>, 2, 2>(src, make_src<kF64, CC, false>(t), ta, 1, q,
-                                                                      oval, oidx, nullptr, st);
+            auto go = [&](auto hsrc) {
+                using H = decltype(hsrc);
+                if (tiled) launch_tiles<S, H, 2, 2, kTileBS>(src, hsrc, ta, 1, q, oval, oidx, nullptr, st);
+                else launch_tiles<S, H, 2, 2, 1024>(src, hsrc, TileArgs{nullptr, a.N, t.N, 0, 1, 0, w.c, w.ctr}, 1, q,
+                                                    oval, oidx, nullptr, st);
+            };
+            if (vec_ok(t, CC)) go(make_src<kF64, CC, true>(t));
+            else go(make_src<kF64, CC, false>(t));
             launched = true;
         }
     });

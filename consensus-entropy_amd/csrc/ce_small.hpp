@@ -23,10 +23,10 @@
 // than 64*W survivors (floods of exact ties at the floor), takes per-wave
 // register lists + a tree merge instead (block-uniform branches, same answer).
 //
-// Merge (S > 1): every thread that wrote list entries fences (release), the
-// block syncs, thread 0 takes a ticket (atomicAdd on the problem's counter);
-// the block that draws S-1 fences (acquire), resets the counter to 0 for the
-// next call, loads the S*q candidates into LDS, and ranks each candidate by
+// Merge (S > 1): the tile lists are stored write-through and every tile
+// arrives on its problem's counter (arrive_last, ce_stream.hpp: no L2
+// write-back / invalidate); the last tile to arrive resets the counter for
+// the next call, loads the S*q candidates into LDS (sc1 loads), and ranks each candidate by
 // its slot in its own list + a binary search in each other list (all lists
 // are best-first; empty slots -- key 0, idx -1 -- sort after every real
 // candidate).  Counters live in the workspace header: zero before the first
@@ -36,24 +36,6 @@
 #include "ce_stream.hpp"
 
 namespace ce {
-
-template <int GS>
-__device__ __forceinline__ void group_best(uint64_t& k, int64_t& i) {
-    uint64_t pk;
-    int64_t pi;
-#define CE_GB(J)                    \
-    if constexpr (GS > J) {         \
-        pk = k;                     \
-        pi = i;                     \
-        xor_cand<J>(pk, pi);        \
-        if (better(pk, pi, k, i)) { \
-            k = pk;                 \
-            i = pi;                 \
-        }                           \
-    }
-    CE_GB(1) CE_GB(2) CE_GB(4) CE_GB(8)
-#undef CE_GB
-}
 
 #ifdef CE_PHASE_TIMING
 // diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
@@ -100,13 +82,15 @@ struct TileSmem {
     };
 };
 
-// Keys of this thread's IPT items lo + tid + BS*v of [lo, hi) (all loads in
-// flight before the arithmetic; `tab` committed once the data is awaited).
-template <class Src, int IPT, int UNR, int BS, int K>
+// Keys of this thread's IPT items lo + tid + BS*v of [lo, hi) into slots
+// [OFF, OFF + IPT) (all loads in flight before the arithmetic; COMMIT: `tab`
+// is committed once the data is awaited -- exactly one tile_keys call of a
+// block commits).  Slots outside [OFF, OFF + IPT) are left as they are.
+template <class Src, int IPT, int UNR, int BS, int K, int OFF, bool COMMIT>
 __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi, int64_t rel, const uint32_t* excl,
                                           LogTablePrefetch& tab, uint64_t (&k)[K], int64_t (&pos)[K],
                                           bool (&ok)[K]) {
-    static_assert(IPT <= K, "");
+    static_assert(OFF + IPT <= K, "");
     const int tid = threadIdx.x, w = tid >> 6;
     const int64_t len = hi - lo;
     int64_t items[IPT];
@@ -120,22 +104,17 @@ __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi
         nlive += (int64_t)BS * v + 64 * w < len;
     }
     if (len > 0) {  // block-uniform
-        src.template keys_small<UNR, IPT>(items, kk, nlive, [&]() { tab.commit(); });
-    } else {
+        if constexpr (COMMIT) src.template keys_small<UNR, IPT>(items, kk, nlive, [&]() { tab.commit(); });
+        else src.template keys_small<UNR, IPT>(items, kk, nlive);
+    } else if constexpr (COMMIT) {
         tab.commit();
     }
 #pragma unroll
-    for (int v = 0; v < K; ++v) {
-        if (v < IPT) {
-            k[v] = kk[v];
-            pos[v] = items[v] + rel;
-            ok[v] = tid + (int64_t)BS * v < len;
-            if (excl) ok[v] = ok[v] && !excluded(excl, items[v]);
-        } else {
-            k[v] = 0;
-            pos[v] = INT64_MAX;
-            ok[v] = false;
-        }
+    for (int v = 0; v < IPT; ++v) {
+        k[OFF + v] = kk[v];
+        pos[OFF + v] = items[v] + rel;
+        ok[OFF + v] = tid + (int64_t)BS * v < len;
+        if (excl) ok[OFF + v] = ok[OFF + v] && !excluded(excl, items[v]);
     }
 }
 
@@ -144,7 +123,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     SrcA srcA, SrcB srcB, TileArgs ta, int q, double* __restrict__ oval, int64_t* __restrict__ oidx,
     const uint32_t* __restrict__ excl) {
     constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
-    constexpr int K = IPTA > IPTB ? IPTA : IPTB;
+    constexpr int K = IPTA + IPTB;  // slots: segment A's, then segment B's (both segments in one block)
     static_assert(BS % 64 == 0 && BS >= 128 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
     using SM = TileSmem<W>;
     __shared__ SM sm;
@@ -159,6 +138,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int64_t rel = (ta.offsets ? 0 : ta.base_idx) - s0;  // A: position = item + rel
     const int64_t relB = ta.n + ta.base_idx;                  // B: position = row + relB
     const bool segB = IPTB > 0 && t >= ta.SA;                 // block-uniform
+    // the mix in ONE block (SB == 0 with a segment B): the block takes every
+    // committee item AND every hc row (slots [0, IPTA) and [IPTA, K))
+    const bool both = IPTB > 0 && ta.SB == 0 && ta.nB > 0;
     int64_t lo, hi;
     if (!segB) {
         const int64_t per = (lenA + ta.SA - 1) / ta.SA;
@@ -177,34 +159,53 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     CE_DASSERT(q >= 1 && q <= 64);
     CE_DASSERT(direct || (int64_t)S * q <= kTileMergeCap);
 
-    if (hi - lo > (int64_t)BS * (segB ? IPTB : IPTA)) {  // long tile: per-wave streams + tree merge
+    const bool long_tile = both ? (hi - lo > (int64_t)BS * IPTA || ta.nB > (int64_t)BS * IPTB)
+                                : hi - lo > (int64_t)BS * (segB ? IPTB : IPTA);
+    if (long_tile) {  // block-uniform: per-wave streams + tree merge
         tab.commit();
         constexpr int64_t kIt = 64 * 2;
         RegTopQ tq;
         tq.init(q);
-        const int64_t its = (hi - lo + kIt - 1) / kIt, its_w = (its + W - 1) / W;
-        int64_t wlo = lo + (int64_t)w * its_w * kIt;
-        int64_t whi = wlo + its_w * kIt < hi ? wlo + its_w * kIt : hi;
-        if (wlo > whi) wlo = whi;
+        auto wave_part = [&](int64_t a0, int64_t a1, int64_t& wlo, int64_t& whi) {
+            const int64_t its = (a1 - a0 + kIt - 1) / kIt, its_w = (its + W - 1) / W;
+            wlo = a0 + (int64_t)w * its_w * kIt;
+            whi = wlo + its_w * kIt < a1 ? wlo + its_w * kIt : a1;
+            if (wlo > whi) wlo = whi;
+        };
+        int64_t wlo, whi;
+        wave_part(lo, hi, wlo, whi);
         if (!segB) {
             stream_direct_range<SrcA, 2, UNRA>(srcA, wlo, whi, rel, q, tq, excl);
         } else {
+            if constexpr (IPTB > 0) stream_direct_range<SrcB, 2, UNRB>(srcB, wlo, whi, relB, q, tq, nullptr);
+        }
+        if (both) {
+            wave_part(0, ta.nB, wlo, whi);
             if constexpr (IPTB > 0) stream_direct_range<SrcB, 2, UNRB>(srcB, wlo, whi, relB, q, tq, nullptr);
         }
         if (direct) {
             block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
             return;
         }
-        block_merge_write<W>(tq, sm.lists, q, lst, 0);
+        block_merge_write<W>(tq, sm.lists, q, lst, 0, nullptr, nullptr, W, true);
     } else {
         // 1. keys of this thread's items
         uint64_t k[K];
         int64_t pos[K];
         bool ok[K];
+#pragma unroll
+        for (int v = 0; v < K; ++v) {
+            k[v] = 0;
+            pos[v] = INT64_MAX;
+            ok[v] = false;
+        }
         if (!segB) {
-            tile_keys<SrcA, IPTA, UNRA, BS, K>(srcA, lo, hi, rel, excl, tab, k, pos, ok);
+            tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, rel, excl, tab, k, pos, ok);
+            if constexpr (IPTB > 0)
+                if (both) tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, false>(srcB, 0, ta.nB, relB, nullptr, tab, k, pos, ok);
         } else {
-            if constexpr (IPTB > 0) tile_keys<SrcB, IPTB, UNRB, BS, K>(srcB, lo, hi, relB, nullptr, tab, k, pos, ok);
+            if constexpr (IPTB > 0)
+                tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, true>(srcB, lo, hi, relB, nullptr, tab, k, pos, ok);
         }
         CE_STAMP(blockIdx.x, 1)
         uint64_t bk = 0;
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                         ov[r] = key_to_val(mk);
                         oi[r] = mi;
                     } else {
-                        lst[r] = Cand{mk, mi};
+                        store_cand_wt(lst + r, mk, mi);
                     }
                 }
             } else if (tid < q) {  // fewer survivors than q: padding
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
                     oi[tid] = -1;
                 } else {
-                    lst[tid] = Cand{0ull, -1};
+                    store_cand_wt(lst + tid, 0ull, -1);
                 }
             }
             CE_STAMP(blockIdx.x, 4)
@@ -303,27 +304,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
                 return;
             }
-            block_merge_write<W>(tq, sm.lists, q, lst, 0);
+            block_merge_write<W>(tq, sm.lists, q, lst, 0, nullptr, nullptr, W, true);
         }
     }
 
     // ---- arrival ticket: the last tile of problem p merges the S lists ----
-    __threadfence();  // release this tile's list (every writer fences its own stores)
-    __syncthreads();
-    if (tid == 0) sm.ticket = (int)atomicAdd(&ta.ctr[p], 1u);
-    __syncthreads();
-    const int ticket = sm.ticket;
-    CE_DASSERT(ticket >= 0 && ticket < S);
-    if (ticket != S - 1) return;  // block-uniform
-    __threadfence();              // acquire: every other tile's list is visible
-    if (tid == 0) {
-        atomicExch(&ta.ctr[p], 0u);  // every tile of p has arrived: reset for the next call
-        sm.nvalid = 0;
-    }
+    if (!arrive_last(ta.ctr + p, (uint32_t)S, &sm.ticket)) return;  // block-uniform
+    if (tid == 0) sm.nvalid = 0;
     const Cand* L = ta.lists + (int64_t)p * S * q;
     const int nL = S * q;
-    for (int j = tid; j < nL; j += BS) {
-        const Cand c = L[j];
+    for (int j = tid; j < nL; j += BS) {  // handed off in this launch: sc1 loads only
+        const Cand c = load_cand_wt(L + j);
         sm.m.k[j] = c.key;
         sm.m.i[j] = c.idx;
     }

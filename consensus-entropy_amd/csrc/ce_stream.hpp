@@ -381,9 +381,46 @@ struct StreamArgs {
 // list in LDS and waves w = 0 mod 2s merge it in (7 shuffle stages); every
 // LDS slot is written once and read once, one barrier per level.
 // nw = waves taking part (a power of two <= WAVES; default all of them).
+// Cross-block hand-off inside one launch (MI355X_MICROARCH.md, "Valid forms",
+// the table's first row): every handed-off byte is stored write-through (sc1:
+// relaxed agent-scope atomic stores), every storing wave waits for its stores
+// (s_waitcnt vmcnt(0)), the block syncs and ONE lane adds to the problem's
+// arrival counter (agent scope); the block whose add returns the last ticket
+// reads the bytes with sc1 loads only (relaxed agent-scope atomic loads).  No
+// L2 write-back or invalidate: a __threadfence() per block (buffer_wbl2 +
+// buffer_inv) made the 1000-block batched launch 118 us instead of ~14.
+__device__ __forceinline__ void store_cand_wt(Cand* p, uint64_t k, int64_t i) {
+    __hip_atomic_store(&p->key, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&p->idx, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Cand load_cand_wt(const Cand* p) {
+    Cand c;
+    c.key = __hip_atomic_load(&p->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c.idx = __hip_atomic_load(&p->idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return c;
+}
+// Every thread of the block calls it after its write-through stores; true in
+// every thread of the block whose arrival is the n-th (that block resets the
+// counter to 0 for the next call: all n arrivals have happened).
+__device__ __forceinline__ bool arrive_last(uint32_t* ctr, uint32_t n, int* lds_ticket) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *lds_ticket = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = *lds_ticket;
+    CE_DASSERT(t >= 0 && t < (int)n);
+    const bool last = t == (int)n - 1;
+    if (last && threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return last;
+}
+
+// wt: the list at wc is read inside this launch (a fold / tile merge): store
+// it write-through (store_cand_wt).
 template <int WAVES>
 __device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L, int q, Cand* wc, int nlists,
-                                         double* oval = nullptr, int64_t* oidx = nullptr, int nw = WAVES) {
+                                         double* oval = nullptr, int64_t* oidx = nullptr, int nw = WAVES,
+                                         bool wt = false) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // empty lists for the workspace slots no block of this (occupancy-sized)
     // grid owns: b + gridDim.x, b + 2*gridDim.x, ...
@@ -415,6 +452,8 @@ __device__ inline void block_merge_write(const RegTopQ& tq, WaveListsT<WAVES>& L
         if (oval) {
             oval[lane] = ok ? key_to_val(k) : __longlong_as_double(0x7ff8000000000000ll);
             oidx[lane] = ok ? i : -1;
+        } else if (wt) {
+            store_cand_wt(wc + lane, ok ? k : 0ull, ok ? i : -1);
         } else {
             wc[lane] = Cand{ok ? k : 0ull, ok ? i : -1};
         }
@@ -456,7 +495,8 @@ struct FoldSrc {
     int64_t na_q;  // na * q
     const Cand* extra;
     __device__ __forceinline__ void get(int64_t j, uint64_t& k, int64_t& i) const {
-        const Cand x = j < na_q ? a[j] : extra[j - na_q];
+        // the grid's lists were handed off in this launch: sc1 loads only
+        const Cand x = j < na_q ? load_cand_wt(a + j) : extra[j - na_q];
         k = x.key;
         i = x.idx;
     }
@@ -510,27 +550,181 @@ __device__ inline void merge_lists_block(Src src, int64_t seg0, int nl, int q, W
 }
 
 // Arrival ticket of a stage-1 grid (a.ctr != nullptr: stage 2 folded into
-// stage 1): after its list is written, every block fences (release) and
-// takes a ticket; the block that draws gridDim.x - 1 fences (acquire), resets
-// the counter and merges the grid's lists into the final output / records.
+// stage 1): after its list is written (write-through), every block arrives;
+// the last to arrive resets the counter and merges the grid's lists into the
+// final output / records.
+// The best (k, i) of each group of GS lanes in all its lanes (butterfly).
+template <int GS>
+__device__ __forceinline__ void group_best(uint64_t& k, int64_t& i) {
+    uint64_t pk;
+    int64_t pi;
+#define CE_GB(J)                    \
+    if constexpr (GS > J) {         \
+        pk = k;                     \
+        pi = i;                     \
+        xor_cand<J>(pk, pi);        \
+        if (better(pk, pi, k, i)) { \
+            k = pk;                 \
+            i = pi;                 \
+        }                           \
+    }
+    CE_GB(1) CE_GB(2) CE_GB(4) CE_GB(8)
+#undef CE_GB
+}
+
+// The fold's merge, one block of W waves over nl <= 64 * W * kLeanJ lists
+// handed off in this launch (sc1 loads), in two rounds of loads:
+//   1. every thread loads the heads of its lists (t, t + 64W, ...); the best
+//      head per group of W lanes gives 64 group bests -- heads of 64 distinct
+//      lists -- and the one of rank q-1 is an exact floor T (q lists hold an
+//      entry >= T, so every global top-q candidate is >= T); none when fewer
+//      than q groups hold a list;
+//   2. the lists whose head is >= T (~q of them) are appended to an LDS
+//      index; their q entries are loaded at once (one per thread), those >= T
+//      appended to a survivor list, and every survivor takes the output slot
+//      of its rank among the survivors.
+// More than 64 * W qualifying-list entries or survivors (floods of ties at
+// T): the register-list merge (merge_lists_block) instead.  Round 2 of this
+// round measured the register-list merge at ~20 us as the last block of the
+// 100M-item grid (sequential per-list loads, sort networks on cold lists).
+constexpr int kLeanJ = 8;
+template <int W>
+struct LeanMergeSmem {
+    uint64_t gk[64];
+    int64_t gi[64];
+    int part[W][64];
+    int lists[64 * W];
+    int nlists, nsurv, ticket;
+    uint64_t bk[W];
+    int64_t bi[W];
+};
+
+template <int W, class Src>
+__device__ inline void merge_lists_lean(Src src, int nl, int q, WaveListsT<W>& L, LeanMergeSmem<W>& sm,
+                                        double* oval, int64_t* oidx, Cand* ocand) {
+    constexpr int BS = 64 * W, GS = W;  // lanes per group: 64 groups
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    uint64_t* sk = &L.key[0][0];  // survivors: the block-merge scratch, 64 W slots
+    int64_t* si = &L.idx[0][0];
+    // 1. heads, all loads in flight
+    uint64_t hk[kLeanJ];
+    int64_t hi[kLeanJ];
+#pragma unroll
+    for (int j = 0; j < kLeanJ; ++j) {
+        hk[j] = 0;
+        hi[j] = INT64_MAX;
+        const int g = tid + BS * j;
+        if (g < nl) src.get((int64_t)g * q, hk[j], hi[j]);
+    }
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+#pragma unroll
+    for (int j = 0; j < kLeanJ; ++j) {
+        if (hi[j] < 0) hi[j] = INT64_MAX;  // empty list: no head
+        if (hi[j] != INT64_MAX && better(hk[j], hi[j], bk, bi)) {
+            bk = hk[j];
+            bi = hi[j];
+        }
+    }
+    group_best<GS>(bk, bi);
+    if ((tid & (GS - 1)) == 0) {
+        sm.gk[tid / GS] = bk;
+        sm.gi[tid / GS] = bi;
+    }
+    if (tid == 0) {
+        sm.nlists = 0;
+        sm.nsurv = 0;
+    }
+    __syncthreads();
+    {
+        const uint64_t mk = sm.gk[lane];
+        const int64_t mi = sm.gi[lane];
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < 64 / W; ++j) {
+            const int o = w * (64 / W) + j;
+            r += better(sm.gk[o], sm.gi[o], mk, mi);
+        }
+        sm.part[w][lane] = r;
+    }
+    __syncthreads();
+    uint64_t fk = 0;  // no floor: admit everything
+    int64_t fi = INT64_MAX;
+    {
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) r += sm.part[j][lane];
+        const uint64_t hit = __ballot(r == q - 1 && sm.gi[lane] != INT64_MAX);
+        if (hit) {
+            const int sl = __builtin_ctzll(hit);
+            fk = sm.gk[sl];
+            fi = sm.gi[sl];
+        }
+    }
+    // 2. lists whose head is >= T
+#pragma unroll
+    for (int j = 0; j < kLeanJ; ++j) {
+        if (hi[j] != INT64_MAX && !better(fk, fi, hk[j], hi[j])) {
+            const int s = atomicAdd(&sm.nlists, 1);
+            if (s < BS) sm.lists[s] = tid + BS * j;
+        }
+    }
+    __syncthreads();
+    const int nq = sm.nlists;
+    if (nq * q > BS) {  // block-uniform: floods of ties at T -> the register-list merge
+        merge_lists_block<W>(src, 0, nl, q, L, sm.bk, sm.bi, oval, oidx, ocand);
+        return;
+    }
+    if (tid < nq * q) {
+        const int li = sm.lists[tid / q], e = tid - (tid / q) * q;
+        uint64_t ck;
+        int64_t ci;
+        src.get((int64_t)li * q + e, ck, ci);
+        if (ci >= 0 && !better(fk, fi, ck, ci)) {
+            const int s = atomicAdd(&sm.nsurv, 1);
+            sk[s] = ck;
+            si[s] = ci;
+        }
+    }
+    __syncthreads();
+    const int ns = sm.nsurv;
+    if (tid < ns) {
+        const uint64_t mk = sk[tid];
+        const int64_t mi = si[tid];
+        int r = 0;
+        for (int j = 0; j < ns; ++j) r += better(sk[j], si[j], mk, mi);
+        if (r < q) {
+            if (ocand) {
+                ocand[r] = Cand{mk, mi};
+            } else {
+                oval[r] = key_to_val(mk);
+                oidx[r] = mi;
+            }
+        }
+    }
+    for (int r = ns + tid; r < q; r += BS) {  // fewer candidates than q: padding
+        if (ocand) {
+            ocand[r] = Cand{0ull, -1};
+        } else {
+            oval[r] = __longlong_as_double(0x7ff8000000000000ll);
+            oidx[r] = -1;
+        }
+    }
+}
+
 template <int W>
 __device__ inline void fold_merge(uint32_t* ctr, double* oval, int64_t* oidx, Cand* ocand, int q, const Cand* wc0,
                                   WaveListsT<W>& L, const Cand* extra = nullptr) {
-    __shared__ int ticket;
-    __shared__ uint64_t bk[W];
-    __shared__ int64_t bi[W];
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) ticket = (int)atomicAdd(ctr, 1u);
-    __syncthreads();
-    CE_DASSERT(ticket >= 0 && ticket < (int)gridDim.x);
-    if (ticket != (int)gridDim.x - 1) return;  // block-uniform
-    __threadfence();
-    if (threadIdx.x == 0) atomicExch(ctr, 0u);
-    // extra (a chunked job's running list) may be ocand itself: every input is in
-    // registers before block_merge_write stores the result
-    merge_lists_block<W>(FoldSrc{wc0, (int64_t)gridDim.x * q, extra}, 0, (int)gridDim.x + (extra ? 1 : 0), q, L, bk,
-                         bi, oval, oidx, ocand);
+    __shared__ LeanMergeSmem<W> ms;
+    if (!arrive_last(ctr, gridDim.x, &ms.ticket)) return;  // block-uniform
+    // extra (a chunked job's running list) may be ocand itself: every input is
+    // read before the outputs are written (barriers in between)
+    const int nl = (int)gridDim.x + (extra ? 1 : 0);
+    const FoldSrc src{wc0, (int64_t)gridDim.x * q, extra};
+    if (nl <= 64 * W * kLeanJ)
+        merge_lists_lean<W>(src, nl, q, L, ms, oval, oidx, ocand);
+    else
+        merge_lists_block<W>(src, 0, nl, q, L, ms.bk, ms.bi, oval, oidx, ocand);
 }
 
 // Item-major, dense rows of 16*S bytes, LDS-DMA staged (AUX: DMA cache policy);
@@ -575,7 +769,7 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
         if (a.excl) ok = ok && !excluded(a.excl, i < hi ? i : hi - 1);
         tq.offer(order_key(h), i + a.base_idx, ok);
     }
-    block_merge_write<4>(tq, sm.lists, q, wc + (int64_t)blockIdx.x * q, a.nlists);
+    block_merge_write<4>(tq, sm.lists, q, wc + (int64_t)blockIdx.x * q, a.nlists, nullptr, nullptr, 4, a.ctr != nullptr);
     if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm.lists, a.extra);
 }
 
@@ -619,7 +813,7 @@ __global__ __launch_bounds__(256) void k_stream_direct(Src src, StreamArgs a, in
     RegTopQ tq;
     tq.init(q);
     stream_direct_range<Src, IPL, UNR>(src, lo, hi, a.base_idx, q, tq, a.excl);
-    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists);
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists, nullptr, nullptr, 4, a.ctr != nullptr);
     if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm, a.extra);
 }
 

@@ -99,6 +99,8 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        import torch.distributed as dist
+
         dist.destroy_process_group()
 
 

@@ -93,6 +93,7 @@ small)  # single-block / small-pool configs: one kernel trace per config + PMC p
     step $? "trace $TAG$c"
   done
   P=${PMCCFG:-c3}
+  if [ "$P" != none ]; then
   timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/${TAG}pmc_fetch" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_fetch.log" 2>&1
   step $? "${TAG}pmc fetch"
   timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/${TAG}pmc_write" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_write.log" 2>&1
@@ -101,6 +102,7 @@ small)  # single-block / small-pool configs: one kernel trace per config + PMC p
   step $? "${TAG}pmc sq"
   timeout -s KILL 90 rocprofv3 --pmc TA_TA_BUSY_sum SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/${TAG}pmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_ta.log" 2>&1
   step $? "${TAG}pmc ta"
+  fi
   ;;
 debug)  # the whole GPU suite once on the debug build (device bounds checks: make -C consensus-entropy_amd debug)
   CE_AMD_LIB=$ROOT/tools/_diag/libce_amd_debug.so timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest_gpu_debug.log" 2>&1
