@@ -25,7 +25,7 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, (int64_t)G1 + G2, q);
     if (small_enabled() && q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= kSmallPoolItems && N_h <= kSmallPoolItems &&
-        (C == 4 || C == 8)) {
+        C == 4) {
         // both segments in ONE launch: tiles of either segment, ticketed merge (k_select_tiles)
         const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
         if (launch_small_mix(a, t, q, val_out, idx_out, w, st)) return check_launch("ce_select_mix");

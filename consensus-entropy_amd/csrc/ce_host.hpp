@@ -242,6 +242,11 @@ static inline StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx)
     s.oidx = nullptr;
     s.ocand = nullptr;
     s.extra = nullptr;
+    static const int ileave = [] {
+        const char* e = getenv("CE_AMD_ILEAVE");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    s.ileave = ileave;
     return s;
 }
 

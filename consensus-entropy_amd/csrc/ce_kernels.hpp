@@ -56,6 +56,7 @@ struct CommitteeSrc {
     bool pow2;
     static constexpr int kC = C;
     static constexpr int kDT = DT;
+    static constexpr bool kVec = VEC;
     static constexpr int kUnr = DT == kF64 ? 4 : 8;
     __device__ __forceinline__ void mean(int64_t i, double (&m)[C]) const {
         committee_mean<DT, C, VEC, kUnr>(p, i * sN, M, sM, sC, dM, invM, pow2, m);

@@ -13,6 +13,11 @@ template <class Src>
 constexpr int small_ipt() { return Src::kC > 4 ? 2 : 4; }
 template <class Src, int BS>
 constexpr int small_unr() { return (Src::kDT == kF64 || Src::kC > 4 || BS > 512) ? 2 : 4; }
+// the tiled A/B path is instantiated for the reference's committee shapes only
+// (vectorisable f32 / f64 rows of C = 4): 17 shapes x 3 block sizes of this
+// kernel doubled the library
+template <class Src>
+constexpr bool tiles_built() { return Src::kC == 4 && Src::kVec && Src::kDT != kBF16; }
 
 // Default: ONE block per problem (S = 1: the whole pool / user / mix selected
 // by one block, no hand-off).  Measured on MI355X (profiles/r03_small.json):
@@ -50,10 +55,11 @@ static int tiles_for(int64_t len, int64_t target, int q, int smax) {
     return (int)(s < 1 ? 1 : s);
 }
 
-template <class SrcA, class SrcB, int IPTA, int IPTB, int BS>
+template <class SrcA, class SrcB, int IPTA, int IPTB, int BS, int UNRA = small_unr<SrcA, BS>(), bool MERGE = true,
+          bool LONG = true>
 static void launch_tiles(const SrcA& a, const SrcB& b, const TileArgs& ta, int problems, int q, double* oval,
                          int64_t* oidx, const uint32_t* excl, hipStream_t st) {
-    hipLaunchKernelGGL((k_select_tiles<SrcA, SrcB, IPTA, IPTB, small_unr<SrcA, BS>(), 1, BS>),
+    hipLaunchKernelGGL((k_select_tiles<SrcA, SrcB, IPTA, IPTB, UNRA, 1, BS, MERGE, LONG>),
                        dim3((unsigned)(problems * (ta.SA + ta.SB))), dim3(BS), 0, st, a, b, ta, q, oval, oidx, excl);
 }
 
@@ -68,12 +74,18 @@ bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval,
         const int64_t per = cdiv(a.N, SA);
         const TileArgs ta{nullptr, a.N, 0, base_idx, SA, 0, w.c, w.ctr};
         if (SA > 1) {
-            if (per > (int64_t)kTileBS * IPT) return;  // tiles would be long: not this path
-            launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, 1, q, oval, oidx, excl, st);
-        } else if (per <= 512 * IPT) {
-            launch_tiles<S, S, IPT, 0, 512>(src, src, ta, 1, q, oval, oidx, excl, st);
+            if constexpr (tiles_built<S>()) {
+                if (per > (int64_t)kTileBS * IPT) return;  // tiles would be long: not this path
+                launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, 1, q, oval, oidx, excl, st);
+            } else {
+                return;
+            }
+        } else if (per <= 512 * IPT) {  // one block; the pool fits it: no merge, no long path
+            launch_tiles<S, S, IPT, 0, 512, small_unr<S, 512>(), false, false>(src, src, ta, 1, q, oval, oidx, excl,
+                                                                                st);
         } else if (per <= 1024 * IPT) {
-            launch_tiles<S, S, IPT, 0, 1024>(src, src, ta, 1, q, oval, oidx, excl, st);
+            launch_tiles<S, S, IPT, 0, 1024, small_unr<S, 1024>(), false, false>(src, src, ta, 1, q, oval, oidx, excl,
+                                                                                  st);
         } else {
             return;
         }
@@ -100,11 +112,16 @@ bool launch_small_users(const CommArgs& a, const int64_t* offsets, int U, int q,
         const int64_t per = cdiv(cdiv(a.N, U), SA);
         const TileArgs ta{offsets, 0, 0, 0, SA, 0, w.c, w.ctr};
         if (SA > 1) {
-            if (per > (int64_t)kTileBS * IPT) return;
-            launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, U, q, oval, oidx, nullptr, st);
+            if constexpr (tiles_built<S>()) {
+                if (per > (int64_t)kTileBS * IPT) return;
+                launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, U, q, oval, oidx, nullptr, st);
+            } else {
+                return;
+            }
         } else {  // one 512-thread block per user: 2 per CU, all 500 users of configs[2] resident
             if (per > (int64_t)512 * IPT) return;
-            launch_tiles<S, S, IPT, 0, 512>(src, src, ta, U, q, oval, oidx, nullptr, st);
+            launch_tiles<S, S, IPT, 0, 512, small_unr<S, 512>(), false, true>(src, src, ta, U, q, oval, oidx, nullptr,
+                                                                               st);
         }
         launched = true;
     });
@@ -125,14 +142,22 @@ bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, double* oval,
     bool launched = false;
     const int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
-        if constexpr (S::kC == 4 || S::kC == 8) {
+        if constexpr (S::kC == 4) {  // the reference's 4 quadrants (other C: the streaming engine + merge)
             constexpr int CC = S::kC;
+            // committee loads: all of an item's members in one batch for f32 C = 4 (UNR 4), as round 2's
+            // one-block mix (a 16-wave block with UNR 2 measured 12.2 vs 10.0 us at C2)
+            constexpr int UNRA = (S::kDT == kF64 || S::kC > 4) ? 2 : 4;
             auto go = [&](auto hsrc) {
                 using H = decltype(hsrc);
-                if (tiled) launch_tiles<S, H, 2, 2, kTileBS>(src, hsrc, ta, 1, q, oval, oidx, nullptr, st);
-                else launch_tiles<S, H, 2, 2, 1024>(src, hsrc, TileArgs{nullptr, a.N, t.N, 0, 1, 0, w.c, w.ctr}, 1, q,
-                                                    oval, oidx, nullptr, st);
+                if (tiled) {
+                    if constexpr (tiles_built<S>())
+                        launch_tiles<S, H, 2, 2, kTileBS, UNRA>(src, hsrc, ta, 1, q, oval, oidx, nullptr, st);
+                } else {
+                    launch_tiles<S, H, 2, 2, 1024, UNRA, false, false>(
+                        src, hsrc, TileArgs{nullptr, a.N, t.N, 0, 1, 0, w.c, w.ctr}, 1, q, oval, oidx, nullptr, st);
+                }
             };
+            if (tiled && !tiles_built<S>()) return;
             if (vec_ok(t, CC)) go(make_src<kF64, CC, true>(t));
             else go(make_src<kF64, CC, false>(t));
             launched = true;

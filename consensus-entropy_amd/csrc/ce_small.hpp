@@ -118,7 +118,11 @@ __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi
     }
 }
 
-template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS>
+// MERGE: launched with S > 1 tiles per problem (the ticketed merge is compiled
+// in); LONG: a tile may exceed BS * IPT items (the per-wave streaming path is
+// compiled in).  Single-block launches whose host checks bound the problem
+// (one pool, the mix) drop both -- half the code of the kernel.
+template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS, bool MERGE = true, bool LONG = true>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_select_tiles(
     SrcA srcA, SrcB srcB, TileArgs ta, int q, double* __restrict__ oval, int64_t* __restrict__ oidx,
     const uint32_t* __restrict__ excl) {
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         hi = lo + per < ta.nB ? lo + per : ta.nB;
     }
     if (lo > hi) lo = hi;
-    const bool direct = S == 1;  // the tile is the whole problem: final outputs, no merge
+    const bool direct = !MERGE || S == 1;  // the tile is the whole problem: final outputs, no merge
     double* ov = oval + (int64_t)p * q;
     int64_t* oi = oidx + (int64_t)p * q;
     Cand* lst = ta.lists + (int64_t)blockIdx.x * q;
@@ -161,7 +165,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
     const bool long_tile = both ? (hi - lo > (int64_t)BS * IPTA || ta.nB > (int64_t)BS * IPTB)
                                 : hi - lo > (int64_t)BS * (segB ? IPTB : IPTA);
-    if (long_tile) {  // block-uniform: per-wave streams + tree merge
+    CE_DASSERT(LONG || !long_tile);
+    if (LONG && long_tile) {  // block-uniform: per-wave streams + tree merge
         tab.commit();
         constexpr int64_t kIt = 64 * 2;
         RegTopQ tq;
@@ -309,6 +314,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
 
     // ---- arrival ticket: the last tile of problem p merges the S lists ----
+    if constexpr (!MERGE) return;
     if (!arrive_last(ta.ctr + p, (uint32_t)S, &sm.ticket)) return;  // block-uniform
     if (tid == 0) sm.nvalid = 0;
     const Cand* L = ta.lists + (int64_t)p * S * q;

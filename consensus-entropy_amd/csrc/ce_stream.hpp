@@ -366,6 +366,7 @@ struct StreamArgs {
     int64_t per_wave;  // items per wave (multiple of 64)
     const uint32_t* excl;  // exclusion bitmap over items 0..N-1 (1 = out of the pool), or nullptr
     int nlists;        // workspace lists (>= gridDim.x); lists past the grid are written empty
+    int ileave;        // k_stream_nmc: the block's waves interleave 64-item tiles (A/B knob CE_AMD_ILEAVE)
     // stage 2 folded in (ctr != nullptr): the last block merges the grid's
     // lists into (oval, oidx), or into q records at ocand
     uint32_t* ctr;
@@ -736,10 +737,17 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     CE_DASSERT((int)gridDim.x <= a.nlists && q >= 1 && q <= kStreamMaxQ);
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t gw = (int64_t)blockIdx.x * 4 + w;
-    int64_t lo = gw * a.per_wave;
-    int64_t hi = lo + a.per_wave;
-    if (hi > a.N) hi = a.N;
+    int64_t lo, hi, step;
+    if (a.ileave) {  // the block's 4 waves take alternate tiles of the block's run (adjacent bursts per member row)
+        const int64_t blo = (int64_t)blockIdx.x * 4 * a.per_wave;
+        hi = blo + 4 * a.per_wave < a.N ? blo + 4 * a.per_wave : a.N;
+        lo = blo + 64 * w;
+        step = 256;
+    } else {  // each wave a contiguous run
+        lo = ((int64_t)blockIdx.x * 4 + w) * a.per_wave;
+        hi = lo + a.per_wave < a.N ? lo + a.per_wave : a.N;
+        step = 64;
+    }
     if (lo > hi) lo = hi;
     RegTopQ tq;
     tq.init(q);
@@ -753,13 +761,13 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     };
     ItemTile<S> t;
     if (lo < hi) issue(lo, (int)min<int64_t>(64, hi - lo));
-    for (int64_t t0 = lo; t0 < hi; t0 += 64) {
+    for (int64_t t0 = lo; t0 < hi; t0 += step) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (MNC) t.read_mnc(lds);
         else t.read(lds);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        const int64_t t1 = t0 + 64;
+        const int64_t t1 = t0 + step;
         if (t1 < hi) issue(t1, (int)min<int64_t>(64, hi - t1));
         double mean[C];
         t.template mean<DT, C>(a.dM, a.invM, a.pow2, mean);
