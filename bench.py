@@ -49,7 +49,7 @@ TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 # the stage-1 kernel each layout launches at M=16, C=4, f32, q <= 64 (ce_kernels.hip launch_stream)
 STAGE1_KERNEL = {
     "NMC": "ce::k_stream_nmc<f32, C=4, S=16> (item-major, LDS-DMA tiles; stage 2 folded into the last block)",
-    "MNC": "ce::k_stream_direct<CommitteeSrc<f32, C=4, vec>, IPL=2, UNR=8> (member-major, direct loads; stage 2 folded)",
+    "MNC": "ce::k_stream_nmc<f32, C=4, S=16, member-major> (member-major, LDS-DMA tiles of one 1 KiB run per member; stage 2 folded)",
 }
 
 

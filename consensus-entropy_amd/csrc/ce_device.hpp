@@ -138,12 +138,58 @@ struct RowDivisor {
     }
 };
 
+// The row's C quotients x[c] / s with ONE range test for the whole row
+// (-DCE_ROWDIV): when every x[c] and s is positive with its exponent field in
+// [723, 1323) -- [2^-300, 2^300) -- both v_div_scale steps return their
+// inputs (no operand is zero, tiny or huge, quotient exponents differ by
+// < 768), v_div_fmas is a plain fma and v_div_fixup returns its input, so
+// x / s == fma(fma(-s, q, x), r, q), q = x * r, with r the division's own
+// refined reciprocal of s: one reciprocal per row, 3 instructions per class
+// instead of ~11.  Rows with a zero, a tiny or a negative value (and NaN /
+// inf) take the ordinary divisions.  The range test is two min/max folds of
+// the high words and one compare.
+template <int C>
+__device__ __forceinline__ void row_quotients(const double (&x)[C], double s, double (&d)[C]) {
+#ifdef CE_ROWDIV
+    const uint32_t hs = (uint32_t)(dbits(s) >> 32);
+    uint32_t lo = hs, hi = hs;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t h = (uint32_t)(dbits(x[c]) >> 32);
+        lo = lo < h ? lo : h;
+        hi = hi > h ? hi : h;
+    }
+    if (__builtin_expect(lo >= (723u << 20) && hi < (1323u << 20), 1)) {
+        double r = __builtin_amdgcn_rcp(s);
+        r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
+        r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const double q = x[c] * r;
+            d[c] = __builtin_fma(__builtin_fma(-s, q, x[c]), r, q);
+        }
+        return;
+    }
+#endif
+#pragma unroll
+    for (int c = 0; c < C; ++c) d[c] = x[c] / s;
+}
+
 // scipy.stats.entropy of one row held in registers (mean: consensus row).
 template <int C>
 __device__ __forceinline__ double entropy_row(const double (&mean)[C]) {
     const double s = row_sum<C>(mean);
-    const RowDivisor d(s);
     double e[C];
+#if defined(CE_ROWDIV)
+    if constexpr (C <= 8) {
+        double d[C];
+        row_quotients<C>(mean, s, d);
+#pragma unroll
+        for (int c = 0; c < C; ++c) e[c] = entr(d[c]);
+        return row_sum<C>(e);
+    }
+#endif
+    const RowDivisor d(s);
 #pragma unroll
     for (int c = 0; c < C; ++c) e[c] = entr(d.div(1.0 * mean[c]));
     return row_sum<C>(e);
@@ -191,6 +237,10 @@ struct MemberLoad<kF32, C, true> {
 #pragma unroll
         for (int k = 0; k < C / 4; ++k) v[k] = __builtin_nontemporal_load(p + k);
     }
+    __device__ __forceinline__ void pin() const {
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) asm volatile("" ::"v"(v[k]));
+    }
     __device__ __forceinline__ void add_to(double (&acc)[C]) const {
 #pragma unroll
         for (int k = 0; k < C / 4; ++k) {
@@ -220,6 +270,10 @@ struct MemberLoad<kF64, C, true> {
 #pragma unroll
         for (int k = 0; k < C / 2; ++k) v[k] = __builtin_nontemporal_load(p + k);
     }
+    __device__ __forceinline__ void pin() const {
+#pragma unroll
+        for (int k = 0; k < C / 2; ++k) asm volatile("" ::"v"(v[k]));
+    }
     __device__ __forceinline__ void add_to(double (&acc)[C]) const {
 #pragma unroll
         for (int k = 0; k < C / 2; ++k) {
@@ -244,6 +298,10 @@ struct MemberLoad<kBF16, C, true> {
         const u32x2* p = reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(base) + off);
 #pragma unroll
         for (int k = 0; k < C / 4; ++k) v[k] = __builtin_nontemporal_load(p + k);
+    }
+    __device__ __forceinline__ void pin() const {
+#pragma unroll
+        for (int k = 0; k < C / 4; ++k) asm volatile("" ::"v"(v[k]));
     }
     __device__ __forceinline__ void add_to(double (&acc)[C]) const {
 #pragma unroll
@@ -280,6 +338,10 @@ struct MemberLoad<DT, C, false> {
             else
                 v[c] = bf16_to_f64(static_cast<const uint16_t*>(base)[o]);
         }
+    }
+    __device__ __forceinline__ void pin() const {
+#pragma unroll
+        for (int c = 0; c < C; ++c) asm volatile("" ::"v"(v[c]));
     }
     __device__ __forceinline__ void add_to(double (&acc)[C]) const {
 #pragma unroll

@@ -47,6 +47,13 @@ struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
 
+// item slots a lane keeps in flight in the single-block pools (keys_small);
+// 0 = all of them at once (A/B builds: -DCE_SMALL_THR=1/2)
+#ifndef CE_SMALL_THR
+#define CE_SMALL_THR 0
+#endif
+constexpr int kSmallThrottle = CE_SMALL_THR;
+
 template <int DT, int C, bool VEC>
 struct CommitteeSrc {
     const void* p;
@@ -77,10 +84,15 @@ struct CommitteeSrc {
     // keys() for latency-bound single-block pools: when the whole committee
     // fits one batch (M <= UNR) the loads are issued item by item and each
     // item's mean + entropy runs as soon as ITS loads have landed, so only the
-    // last item's arithmetic trails the last load.  Items u >= nlive (wave-
+    // last item's arithmetic trails the last load.  Every slot's loads are
+    // issued, also for slots without a real item (their addresses are clamped
+    // to the pool's last item: one cache line per wave): loads under a branch
+    // leave the compiler unable to count them, and it then waits for ALL of
+    // them (vmcnt(0)) before the log table's commit, i.e. before the first
+    // item's arithmetic.  Items u >= nlive (wave-
     // uniform: no lane of the wave owns a real item there) skip the arithmetic
     // (key 0).  hook() as in keys().
-    template <int UNR, int IPL, class Hook = NoHook>
+    template <int UNR, int IPL, class Hook = NoHook, int THR = kSmallThrottle>
     __device__ __forceinline__ void keys_small(const int64_t (&items)[IPL], uint64_t (&k)[IPL], int nlive,
                                                Hook hook = {}) const {
         if (M > UNR) {
@@ -88,16 +100,31 @@ struct CommitteeSrc {
             return;
         }
         MemberLoad<DT, C, VEC> ld[IPL][UNR];
-#pragma unroll
-        for (int u = 0; u < IPL; ++u) {
-            if (u >= nlive) break;  // wave-uniform: no load for slots without a real item
+        auto issue = [&](int u) {
 #pragma unroll
             for (int v = 0; v < UNR; ++v) ld[u][v].load(p, items[u] * sN + (int64_t)(v < M ? v : M - 1) * sM, sC);
-        }
+        };
+        // THR item slots in flight per lane (THR < IPL: slot u + THR is issued
+        // only once slot u has landed, so every block keeps a bounded share of
+        // the memory queues instead of all of its bytes at once)
+        constexpr int D = (THR > 0 && THR < IPL) ? THR : IPL;
+#pragma unroll
+        for (int u = 0; u < D; ++u) issue(u);
         hook();
         auto item = [&](auto full) {
 #pragma unroll
             for (int u = 0; u < IPL; ++u) {
+                if constexpr (D < IPL) {
+                    if (u + D < IPL) {
+                        // slot u landed (the asm reads its registers: the compiler waits
+                        // for exactly those loads), then slot u + D is issued; the
+                        // memory clobber keeps that issue behind the wait
+#pragma unroll
+                        for (int v = 0; v < UNR; ++v) ld[u][v].pin();
+                        asm volatile("" ::: "memory");
+                        issue(u + D);
+                    }
+                }
                 k[u] = 0;
                 if (u >= nlive) continue;  // wave-uniform
                 double acc[C];
