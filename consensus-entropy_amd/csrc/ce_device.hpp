@@ -148,6 +148,11 @@ struct RowDivisor {
 // instead of ~11.  Rows with a zero, a tiny or a negative value (and NaN /
 // inf) take the ordinary divisions.  The range test is two min/max folds of
 // the high words and one compare.
+// on by default (measured: C3 14.24 -> 13.36 us with the throttled slots, the
+// C4 stream unchanged); -DCE_NO_ROWDIV builds the plain divisions for A/B
+#if !defined(CE_NO_ROWDIV) && !defined(CE_ROWDIV)
+#define CE_ROWDIV 1
+#endif
 template <int C>
 __device__ __forceinline__ void row_quotients(const double (&x)[C], double s, double (&d)[C]) {
 #ifdef CE_ROWDIV

@@ -188,6 +188,6 @@ bool launch_seg(const CommArgs& a, const int64_t* offsets, int64_t n, int64_t ba
 
 #ifdef CE_PHASE_TIMING
 extern "C" int ce_debug_phase(uint64_t* host, int n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), (size_t)n * 6 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), (size_t)n * 16 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -39,11 +39,16 @@ namespace ce {
 
 #ifdef CE_PHASE_TIMING
 // diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
-__device__ uint64_t g_phase[8192][6];
+// [0] start, [1] wave 0's keys done, [2] floor, [3] append, [4] rank, [5] merge,
+// [6 + w] wave w's keys done (w < 8)
+__device__ uint64_t g_phase[8192][16];
 #define CE_STAMP(b, k) \
     if (threadIdx.x == 0 && (b) < 8192) g_phase[b][k] = wall_clock64();
+#define CE_WSTAMP(b) \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 8 && (b) < 8192) g_phase[b][6 + (threadIdx.x >> 6)] = wall_clock64();
 #else
 #define CE_STAMP(b, k)
+#define CE_WSTAMP(b)
 #endif
 
 // Geometry of a tiled launch: block b is tile t = b % S of problem p = b / S,
@@ -213,6 +218,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, true>(srcB, lo, hi, relB, nullptr, tab, k, pos, ok);
         }
         CE_STAMP(blockIdx.x, 1)
+        CE_WSTAMP(blockIdx.x)
         uint64_t bk = 0;
         int64_t bi = INT64_MAX;
 #pragma unroll

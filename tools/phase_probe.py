@@ -21,7 +21,7 @@ offs = torch.arange(U + 1, device="cuda", dtype=torch.int64) * Nu
 for _ in range(20):
     ops.select_batched(P, offs, 10, "MNC")
 torch.cuda.synchronize()
-buf = np.zeros((U, 6), np.uint64)
+buf = np.zeros((U, 16), np.uint64)
 assert L.ce_debug_phase(buf.ctypes.data_as(ctypes.c_void_p), U) == 0
 t = (buf.astype(np.int64) - int(buf[:, 0].min())) * 10  # ns
 out = {"start_ns": np.percentile(t[:, 0], [0, 25, 50, 75, 100]).tolist(),
@@ -30,5 +30,10 @@ out = {"start_ns": np.percentile(t[:, 0], [0, 25, 50, 75, 100]).tolist(),
        "append_ns": np.percentile(t[:, 3] - t[:, 2], [0, 50, 100]).tolist(),
        "rank_ns": np.percentile(t[:, 4] - t[:, 3], [0, 50, 100]).tolist(),
        "end_ns": np.percentile(t[:, 4], [0, 50, 100]).tolist(),
-       "start_hist": np.histogram(t[:, 0], bins=10)[0].tolist()}
+       "start_hist": np.histogram(t[:, 0], bins=10)[0].tolist(),
+       # per-wave key ends (waves 0..7): the block's slowest / fastest wave, and the intra-block skew
+       "wave_keys_last_ns": np.percentile(t[:, 6:14].max(1) - t[:, 0], [0, 50, 100]).tolist(),
+       "wave_keys_first_ns": np.percentile(t[:, 6:14].min(1) - t[:, 0], [0, 50, 100]).tolist(),
+       "wave_skew_ns": np.percentile(t[:, 6:14].max(1) - t[:, 6:14].min(1), [0, 50, 100]).tolist(),
+       "floor_after_last_wave_ns": np.percentile(t[:, 2] - t[:, 6:14].max(1), [0, 50, 100]).tolist()}
 print(json.dumps(out))
