@@ -165,7 +165,7 @@ def cpu_reference_1thread(only):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="0,1,2,4,5,6,7")
+    ap.add_argument("--only", default="0,1,2,4,5,6,7,8")
     ap.add_argument("--cpu", action="store_true", help="also time the reference expressions on the host")
     args = ap.parse_args()
     only = {int(x) for x in args.only.split(",")}
@@ -244,6 +244,44 @@ def main():
                        f"{'with' if miss else 'no'} missing values", F, F * D * 8, t,
                        {"node_steps_per_s": F * T * depth / t})
             del X
+    if 8 in only:
+        frames_selection_configs(g, report)
+
+
+def frames_selection_configs(g, report_fn, q=10):
+    """SURVEY.md §8(f)1 end to end: three frame-level members (gnb, sgd, xgb:
+    [F, 4] f64 frame rows, amg_test.py:435-437) and one song-level member (the
+    CNN's [N, 4]) -> groupby mean -> member-sequential mean -> entropy -> top-q
+    (:437-445).  Fused: ce_select_frames (one pass, the [M, N, C] stack never
+    written).  Two-step: ce_segment_mean of each frame member into its row of a
+    preallocated [M, N, C] stack + ce_select_mc over the stack.  Frames grouped
+    (CSR) and shuffled (permutation gather)."""
+    for songs, fps in ((1608, 40), (1_000_000, 40)):
+        F, C = songs * fps, 4
+        fr = [dirichlet((F, C), torch.float64, g) for _ in range(3)]
+        cnn = dirichlet((songs, C), torch.float64, g)
+        offs = torch.arange(0, songs + 1, device="cuda", dtype=torch.int64) * fps
+        stack = torch.empty((4, songs, C), device="cuda", dtype=torch.float64)
+        stack[3].copy_(cnn)
+        reps = 200 if songs < 10_000 else 40
+        for perm in (None, torch.randperm(F, device="cuda", generator=g)):
+            kind = "grouped" if perm is None else "permuted"
+            byts = 3 * F * C * 8 + songs * C * 8 + (3 * F * 8 if perm is not None else 0)
+
+            def two_step():
+                for m in range(3):
+                    ops.segment_mean(fr[m], offs, perm, out=stack[m])
+                return ops.select_mc(stack, q, "MNC")
+
+            fused = lambda: ops.select_frames(fr + [cnn], offs, q, perm=perm)  # noqa: E731
+            a, b = fused(), two_step()
+            same = bool(torch.equal(a[1], b[1]) and torch.equal(a[0].view(torch.int64), b[0].view(torch.int64)))
+            t_f = timed(fused, reps)
+            t_2 = timed(two_step, reps)
+            report_fn(f"(f)1 frames -> selection {songs} songs x {fps} frames, 3 frame + 1 song member, {kind}: fused",
+                      songs, byts, t_f, {"same_selection_as_two_step": same})
+            report_fn(f"(f)1 frames -> selection {songs} songs x {fps} frames, 3 frame + 1 song member, {kind}: two-step",
+                      songs, byts, t_2, {"speedup_fused": t_2 / t_f})
 
 
 def segment_mean_configs(g, report_fn):

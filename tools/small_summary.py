@@ -39,7 +39,8 @@ def main(prof, out):
                             "min_us": v[0] / 1e3, "max_us": v[-1] / 1e3}
     try:
         from pmc_reduce import main as pmc_main
-        for tag in ("", "r02_"):
+        tags = sorted({os.path.basename(d)[:-len("pmc_fetch")] for d in glob.glob(os.path.join(prof, "*pmc_fetch"))})
+        for tag in tags:
             passes = [p for p in (f"{tag}pmc_fetch", f"{tag}pmc_write", f"{tag}pmc_sq", f"{tag}pmc_ta")
                       if os.path.isdir(os.path.join(prof, p))]
             if passes:
