@@ -181,6 +181,20 @@ static inline bool dma_nt() {
 }
 
 // A/B knob: CE_AMD_WIDE2=0 -> the unpipelined wide kernel (k_stream_wide)
+// A/B knob: CE_AMD_WIDE_DMA=1 -> the LDS-DMA tile stream (k_stream_wide_dma)
+// instead of the register-ring wide stream (k_stream_wide2).  Off by default:
+// on the C5 job (12M items, 2M-item chunks, one box, alternating runs) it
+// measured 0.760 / 0.752 of HBM against 0.773 / 0.772 -- 16 KiB in flight per
+// wave (128 KiB per CU, 2.7x the register ring's) bought nothing, so the wide
+// stream is not limited by the bytes it keeps in flight
+static inline bool wide_dma_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("CE_AMD_WIDE_DMA");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 static inline bool wide2_enabled() {
     static const bool on = [] {
         const char* e = getenv("CE_AMD_WIDE2");

@@ -113,6 +113,24 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
         constexpr int DT = decltype(dt)::value, NPL = decltype(npl)::value;
         if constexpr (decltype(vec)::value) {
+            // an item's member rows contiguous ([N, M, C], sM == C): LDS-DMA tiles
+            constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
+            constexpr int TMAX = KCH >= 16 ? 1 : 16 / KCH;
+            const int R = a.C * eb;
+            if (wide_dma_enabled() && a.sM == a.C && R <= 16384) {
+                const int T = std::min(TMAX, 16384 / R);
+                const int tile = (T * R + 1023) / 1024 * 1024;
+                const int rowb = wide_lds_doubles(a.C) * 8;
+                const int bufb = (std::max(tile, rowb) + 15) / 16 * 16;
+                const size_t dl = (size_t)4 * bufb;
+                auto kern = dma_nt() ? k_stream_wide_dma<DT, KCH, 2> : k_stream_wide_dma<DT, KCH, 0>;
+                if (dl > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dl);
+                const int grid = resident_grid(kern, dl, G);
+                stream_grid(sa, grid);
+                sa.per_wave = cdiv(a.N, (int64_t)grid * 4);  // whole items
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), dl, st, wa, pl, sa, q, w.c, T, bufb);
+                return;
+            }
             if (wide2_enabled()) {
                 constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
                 // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M

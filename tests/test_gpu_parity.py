@@ -334,6 +334,21 @@ def test_wide_stream_vs_oracle(ce, N, M, C, dt):
     assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
 
 
+def test_wide_dma_stream_vs_oracle():
+    """The LDS-DMA wide stream (k_stream_wide_dma, an A/B build-time-free knob:
+    CE_AMD_WIDE_DMA=1, read once per process) through the same oracle tests as
+    the default register-ring stream, in a child process with the knob set."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, CE_AMD_WIDE_DMA="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.abspath(__file__), "-q", "-x", "-m", "gpu",
+                        "-k", "wide_stream_vs_oracle or chunked_pool_vs_oracle", "-p", "no:cacheprovider"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout
+
+
 @pytest.mark.parametrize("sizes", [[1608] * 37, [1, 64, 65, 0, 5000, 127, 20000, 3], [100_000, 70_000]])
 def test_batched_segments_vs_oracle(ce, sizes):
     """Per-user selection in one launch (16-wave blocks, one per user): ragged
