@@ -203,6 +203,8 @@ def select_frames(members, offsets, q, perm=None, base_idx=0, song_level=None):
     arr = (_Member * len(members))()
     keep = []
     F = perm.numel() if perm is not None else None
+    if F is None:  # a member with other than N rows holds the frames: F without a device read
+        F = next((t.shape[0] for t in members if t.dim() == 2 and t.shape[0] != N), None)
     for m, t in enumerate(members):
         _on_gpu(t, f"member {m}")
         if t.dim() != 2 or t.shape[1] != C or t.dtype not in (torch.float32, torch.float64):
@@ -215,7 +217,7 @@ def select_frames(members, offsets, q, perm=None, base_idx=0, song_level=None):
         elif t.shape[0] != N:
             sl = False
         else:  # N rows: song-level unless there are exactly N frames too
-            if F is None:
+            if F is None:  # every member has N rows: only the offsets tell (one device read)
                 F = int(offsets[-1])
             sl = F != N
         arr[m] = _Member(t.data_ptr(), _DT[t.dtype], 1 if sl else 0, t.stride(0))

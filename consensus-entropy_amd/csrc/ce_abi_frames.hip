@@ -50,11 +50,17 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
         fa.per_wave = (cdiv(N, (int64_t)grid * 4) + 63) / 64 * 64;
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, fa, q, w.c);
     };
+    // C lanes per song (k_frames_lanes: whole-row reads, LDS-DMA tiles for
+    // grouped dense members) where C divides the wave; lane per song otherwise
+    static const bool lanes = [] {  // A/B knob: CE_AMD_FRAMES_LANES=0 -> k_frames_select
+        const char* e = getenv("CE_AMD_FRAMES_LANES");
+        return !(e && e[0] == '0');
+    }();
     switch (C) {
-        case 2: go(k_frames_select<2>); break;
+        case 2: lanes ? go(k_frames_lanes<2>) : go(k_frames_select<2>); break;
         case 3: go(k_frames_select<3>); break;
-        case 4: go(k_frames_select<4>); break;
-        default: go(k_frames_select<8>); break;
+        case 4: lanes ? go(k_frames_lanes<4>) : go(k_frames_select<4>); break;
+        default: lanes ? go(k_frames_lanes<8>) : go(k_frames_select<8>); break;
     }
     return check_launch("ce_select_frames");
 }

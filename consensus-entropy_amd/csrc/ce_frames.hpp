@@ -169,4 +169,129 @@ __global__ __launch_bounds__(256) void k_frames_select(FrameArgs a, int q, Cand*
     if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm);
 }
 
+// The same selection with C lanes per song (lane = (song, class), 64 / C songs
+// per wave step): each lane keeps ONE class's sequential group sum, so the
+// frame rows of the wave's songs are read as whole rows.  Grouped frames (no
+// perm) of a dense member (row = C * size bytes, a multiple of 16) reach the
+// wave by LDS-DMA: the wave's songs own the contiguous rows [off[t0],
+// off[t0 + G]), staged 16 KiB at a time (1 KiB per global_load_lds, fully
+// coalesced) in the wave's LDS tile with the 16-B units XOR-swizzled within
+// 256 B (unit p at p ^ ((p >> 4) & 15)), so the songs of a step -- rows a
+// song length apart -- read distinct banks; every lane then adds its song's
+// rows of the tile in row order (pandas group_mean: NaN skipped, counted
+// cells only).  Shuffled frames (perm), strided or 8-B rows are read by direct
+// loads in batches of 8 rows, as k_segment_mean.  The class means of a song
+// meet by lane shuffles; every lane of the song computes its entropy (the
+// group's lane 0 offers it).  Same values as k_frames_select.
+template <int C>
+__global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* __restrict__ wc) {
+    static_assert(64 % C == 0, "C divides the wave");
+    constexpr int G = 64 / C;  // songs per wave step
+    constexpr int TB = 16384;  // per-wave LDS tile
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    __shared__ WaveLists sm;
+    __shared__ __attribute__((aligned(16))) char tiles[4][TB];
+    CE_DASSERT((int)gridDim.x <= a.nlists && q >= 1 && q <= kStreamMaxQ);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sg = lane / C, c = lane - sg * C;
+    char* tile = tiles[w];
+    const int64_t gw = (int64_t)blockIdx.x * 4 + w;
+    int64_t lo = gw * a.per_wave;
+    int64_t hi = lo + a.per_wave;
+    if (hi > a.N) hi = a.N;
+    if (lo > hi) lo = hi;
+    RegTopQ tq;
+    tq.init(q);
+    for (int64_t t0 = lo; t0 < hi; t0 += G) {
+        const int64_t n = t0 + sg;
+        const bool live = n < hi;
+        const int64_t ng = t0 + G < hi ? t0 + G : hi;  // the step's songs [t0, ng)
+        double acc = 0.0;  // np.add.reduce identity
+        for (int mm = 0; mm < a.M; ++mm) {
+            const FrameMember& fm = a.mem[mm];
+            const int EB = fm.dt == kF64 ? 8 : 4;
+            double mean;
+            if (fm.song_level) {
+                const int64_t o = (live ? n : t0) * fm.ld + c;
+                mean = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o] : (double)static_cast<const float*>(fm.p)[o];
+            } else {
+                const int64_t f0 = live ? a.off[n] : 0, f1 = live ? a.off[n + 1] : 0;
+                CE_DASSERT(f0 >= 0 && f0 <= f1);
+                double s = 0.0;
+                int cnt = 0;
+                const int RB = C * EB;
+                const int64_t R0 = a.off[t0];
+                const int64_t R1 = a.off[ng];
+                // the step's songs tile [R0, R1) (CSR offsets); a wave holding a song outside it
+                // (offsets not monotone) reads its rows directly instead
+                const bool inside = !live || (f0 >= R0 && f1 <= R1);
+                if (!a.perm && fm.ld == C && RB % 16 == 0 && fm.vec && __all(inside)) {  // wave-uniform: LDS-DMA tiles
+                    const int TR = TB / RB;  // rows per tile
+                    const char* mb = static_cast<const char*>(fm.p);
+                    for (int64_t c0 = R0; c0 < R1; c0 += TR) {
+                        const int64_t c1 = c0 + TR < R1 ? c0 + TR : R1;
+                        const int units = (int)(c1 - c0) * RB / 16;
+                        const char* src = mb + c0 * RB;
+                        for (int j = 0; j * 64 < units; ++j) {  // wave-uniform
+                            const int pd = j * 64 + lane;  // LDS unit written by this lane
+                            int ps = pd ^ ((pd >> 4) & 15);  // its source unit (the swizzle is an involution)
+                            ps = ps < units ? ps : units - 1;
+                            CE_DASSERT(j * 1024 + 1024 <= TB);
+                            __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)ps * 16),
+                                                             (void __attribute__((address_space(3)))*)(tile + j * 1024),
+                                                             16, 0, 2);
+                        }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        const int64_t r0 = f0 > c0 ? f0 : c0, r1 = f1 < c1 ? f1 : c1;
+                        for (int64_t r = r0; r < r1; ++r) {  // this lane's song's rows in the tile, in order
+                            const int b = (int)(r - c0) * RB + c * EB;
+                            const int u = b >> 4;
+                            const char* e = tile + ((u ^ ((u >> 4) & 15)) << 4) + (b & 15);
+                            const double v = EB == 8 ? *reinterpret_cast<const double*>(e)
+                                                     : (double)*reinterpret_cast<const float*>(e);
+                            if (v == v) {  // not NaN
+                                s += v;
+                                ++cnt;
+                            }
+                        }
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the next DMA
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                } else {  // direct loads: batches of 8 rows in flight, added in row order
+                    constexpr int B = 8;
+                    for (int64_t fb = f0; fb < f1; fb += B) {
+                        double v[B];
+#pragma unroll
+                        for (int u = 0; u < B; ++u) {
+                            const int64_t f = fb + u < f1 ? fb + u : f1 - 1;
+                            const int64_t r = a.perm ? a.perm[f] : f;
+                            const int64_t o = r * fm.ld + c;
+                            v[u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
+                                                 : (double)static_cast<const float*>(fm.p)[o];
+                        }
+#pragma unroll
+                        for (int u = 0; u < B; ++u)
+                            if (fb + u < f1 && v[u] == v[u]) {
+                                s += v[u];
+                                ++cnt;
+                            }
+                    }
+                }
+                double x = cnt ? s / (double)cnt : __longlong_as_double(0x7ff8000000000000ll);
+                if (fm.dt == kF32) x = (double)(float)x;  // the float32 result column
+                mean = x;
+            }
+            acc += mean;
+        }
+        const double mv = div_members(acc, a.dM, a.invM, a.pow2);
+        double row[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) row[k] = __shfl(mv, sg * C + k);
+        const double h = entropy_row<C>(row);
+        tq.offer(order_key(h), n + a.base_idx, live && c == 0);
+    }
+    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists, nullptr, nullptr, 4, a.ctr != nullptr);
+    if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm);
+}
+
 }  // namespace ce
