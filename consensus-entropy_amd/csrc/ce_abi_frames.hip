@@ -45,9 +45,9 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     fa.oval = val_out;
     fa.oidx = idx_out;
     fa.ocand = nullptr;
-    auto go = [&](auto kern) {
+    auto go = [&](auto kern, int step) {  // step: songs per wave step (64 / lanes per song)
         const int grid = resident_grid(kern, 0, G);
-        fa.per_wave = (cdiv(N, (int64_t)grid * 4) + 63) / 64 * 64;
+        fa.per_wave = (cdiv(N, (int64_t)grid * 4) + step - 1) / step * step;
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, fa, q, w.c);
     };
     // C lanes per song (k_frames_lanes: whole-row reads, LDS-DMA tiles for
@@ -56,11 +56,25 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
         const char* e = getenv("CE_AMD_FRAMES_LANES");
         return !(e && e[0] == '0');
     }();
+    static const int dma_env = [] {  // A/B knob: CE_AMD_FRAMES_DMA=0 / 1 forces direct loads / LDS-DMA tiles
+        const char* e = getenv("CE_AMD_FRAMES_DMA");
+        return e ? (e[0] == '0' ? 0 : 1) : -1;
+    }();
+    // LDS-DMA tiles for grouped frames once every wave runs >= 4 steps: at the
+    // reference's 1608 songs x 40 frames the tile round trips are exposed
+    // (DMA 44.6 us, direct 31.7 us); at 1M songs the tiles win (0.92 vs 1.49 ms)
+    auto lanes_go = [&](auto dma_kern, auto direct_kern, int step) {
+        const int grid = resident_grid(dma_kern, 0, G);
+        const int64_t steps_per_wave = cdiv(cdiv(N, (int64_t)grid * 4), (int64_t)step);
+        const bool dma = !perm_or_null && (dma_env >= 0 ? dma_env == 1 : steps_per_wave >= 4);
+        if (dma) go(dma_kern, step);
+        else go(direct_kern, step);
+    };
     switch (C) {
-        case 2: lanes ? go(k_frames_lanes<2>) : go(k_frames_select<2>); break;
-        case 3: go(k_frames_select<3>); break;
-        case 4: lanes ? go(k_frames_lanes<4>) : go(k_frames_select<4>); break;
-        default: lanes ? go(k_frames_lanes<8>) : go(k_frames_select<8>); break;
+        case 2: lanes ? lanes_go(k_frames_lanes<2, true>, k_frames_lanes<2, false>, 32) : go(k_frames_select<2>, 64); break;
+        case 3: go(k_frames_select<3>, 64); break;
+        case 4: lanes ? lanes_go(k_frames_lanes<4, true>, k_frames_lanes<4, false>, 16) : go(k_frames_select<4>, 64); break;
+        default: lanes ? lanes_go(k_frames_lanes<8, true>, k_frames_lanes<8, false>, 8) : go(k_frames_select<8>, 64); break;
     }
     return check_launch("ce_select_frames");
 }

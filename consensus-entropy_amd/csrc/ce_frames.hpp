@@ -42,7 +42,7 @@ struct FrameArgs {
     double dM, invM;
     bool pow2;
     int64_t base_idx;
-    int64_t per_wave;  // songs per wave (multiple of 64)
+    int64_t per_wave;  // songs per wave (a multiple of the kernel's songs per wave step)
     int nlists;
     uint32_t* ctr;  // fold (last block merges the grid)
     double* oval;
@@ -183,11 +183,13 @@ __global__ __launch_bounds__(256) void k_frames_select(FrameArgs a, int q, Cand*
 // loads in batches of 8 rows, as k_segment_mean.  The class means of a song
 // meet by lane shuffles; every lane of the song computes its entropy (the
 // group's lane 0 offers it).  Same values as k_frames_select.
-template <int C>
+// DMA = false: direct loads only, no LDS tiles -- the 64 KiB of tiles would
+// cap the gather (shuffled frames) at 2 blocks per CU.
+template <int C, bool DMA>
 __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* __restrict__ wc) {
     static_assert(64 % C == 0, "C divides the wave");
     constexpr int G = 64 / C;  // songs per wave step
-    constexpr int TB = 16384;  // per-wave LDS tile
+    constexpr int TB = DMA ? 16384 : 16;  // per-wave LDS tile
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     __shared__ WaveLists sm;
     __shared__ __attribute__((aligned(16))) char tiles[4][TB];
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                 // the step's songs tile [R0, R1) (CSR offsets); a wave holding a song outside it
                 // (offsets not monotone) reads its rows directly instead
                 const bool inside = !live || (f0 >= R0 && f1 <= R1);
-                if (!a.perm && fm.ld == C && RB % 16 == 0 && fm.vec && __all(inside)) {  // wave-uniform: LDS-DMA tiles
+                if (DMA && !a.perm && fm.ld == C && RB % 16 == 0 && fm.vec && __all(inside)) {  // wave-uniform: LDS-DMA tiles
                     const int TR = TB / RB;  // rows per tile
                     const char* mb = static_cast<const char*>(fm.p);
                     for (int64_t c0 = R0; c0 < R1; c0 += TR) {
@@ -243,16 +245,26 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                         }
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         const int64_t r0 = f0 > c0 ? f0 : c0, r1 = f1 < c1 ? f1 : c1;
-                        for (int64_t r = r0; r < r1; ++r) {  // this lane's song's rows in the tile, in order
-                            const int b = (int)(r - c0) * RB + c * EB;
-                            const int u = b >> 4;
-                            const char* e = tile + ((u ^ ((u >> 4) & 15)) << 4) + (b & 15);
-                            const double v = EB == 8 ? *reinterpret_cast<const double*>(e)
-                                                     : (double)*reinterpret_cast<const float*>(e);
-                            if (v == v) {  // not NaN
-                                s += v;
-                                ++cnt;
+                        // this lane's song's rows in the tile, in order: 8 LDS reads in flight,
+                        // then the 8 adds (a read per row would wait out an LDS round trip each);
+                        // rows past r1 re-read the tile's first row and are skipped
+                        for (int64_t rb = r0; rb < r1; rb += 8) {
+                            double v[8];
+#pragma unroll
+                            for (int u8 = 0; u8 < 8; ++u8) {
+                                const int64_t r = rb + u8 < r1 ? rb + u8 : c0;
+                                const int b = (int)(r - c0) * RB + c * EB;
+                                const int u = b >> 4;
+                                const char* e = tile + ((u ^ ((u >> 4) & 15)) << 4) + (b & 15);
+                                v[u8] = EB == 8 ? *reinterpret_cast<const double*>(e)
+                                                : (double)*reinterpret_cast<const float*>(e);
                             }
+#pragma unroll
+                            for (int u8 = 0; u8 < 8; ++u8)
+                                if (rb + u8 < r1 && v[u8] == v[u8]) {  // not NaN
+                                    s += v[u8];
+                                    ++cnt;
+                                }
                         }
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the next DMA
                         __builtin_amdgcn_sched_barrier(0);

@@ -349,6 +349,22 @@ def test_wide_dma_stream_vs_oracle():
     assert " passed" in r.stdout
 
 
+def test_frames_dma_tiles_vs_oracle():
+    """ce_select_frames with the grouped members staged by LDS-DMA tiles
+    (k_frames_lanes<C, true>; by default only pools with >= 4 steps per wave
+    take them) forced on by CE_AMD_FRAMES_DMA=1 in a child process: the fused
+    frame tests against the restated groupby mean + oracle."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, CE_AMD_FRAMES_DMA="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.abspath(__file__), "-q", "-x", "-m", "gpu",
+                        "-k", "frames_fused_selection or frames_to_selection", "-p", "no:cacheprovider"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout
+
+
 @pytest.mark.parametrize("sizes", [[1608] * 37, [1, 64, 65, 0, 5000, 127, 20000, 3], [100_000, 70_000]])
 def test_batched_segments_vs_oracle(ce, sizes):
     """Per-user selection in one launch (16-wave blocks, one per user): ragged
