@@ -98,7 +98,23 @@ struct CommitteeSrc {
     __device__ __forceinline__ void keys_small(const int64_t (&items)[IPL], uint64_t (&k)[IPL], int nlive,
                                                Hook hook = {}) const {
         if (M > UNR) {
-            keys<UNR, IPL>(items, k, hook);
+            // committees larger than one batch: f32 rows keep all IPL items' member
+            // batches in flight (IPL x UNR x 4 VGPRs); f64 rows of C >= 4 would need
+            // twice that, so they go item by item (UNR members in flight)
+            if constexpr (!(DT == kF64 && C >= 4)) {
+                keys<UNR, IPL>(items, k, hook);
+                return;
+            }
+            int64_t one[1] = {items[0]};
+            uint64_t k1[1];
+            keys<UNR, 1>(one, k1, hook);
+            k[0] = k1[0];
+#pragma unroll
+            for (int u = 1; u < IPL; ++u) {
+                one[0] = items[u];
+                keys<UNR, 1>(one, k1);
+                k[u] = k1[0];
+            }
             return;
         }
         MemberLoad<DT, C, VEC> ld[IPL][UNR];

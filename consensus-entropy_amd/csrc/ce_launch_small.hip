@@ -11,8 +11,11 @@ using namespace ce;
 // in flight (f64 / C = 8 rows, and 16-wave blocks, take 2).
 template <class Src>
 constexpr int small_ipt() { return Src::kC > 4 ? 2 : 4; }
+// (f64 C = 4 rows take 4 too since the slot throttle: one item slot of M <= 4
+// members in flight per lane, so keys_small's progressive path runs for the
+// reference's 4-member f64 committee, configs[0])
 template <class Src, int BS>
-constexpr int small_unr() { return (Src::kDT == kF64 || Src::kC > 4 || BS > 512) ? 2 : 4; }
+constexpr int small_unr() { return (Src::kC > 4 || BS > 512) ? 2 : 4; }
 // the tiled A/B path is instantiated for the reference's committee shapes only
 // (vectorisable f32 / f64 rows of C = 4): 17 shapes x 3 block sizes of this
 // kernel doubled the library
@@ -81,6 +84,15 @@ bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval,
                 return;
             }
         } else if (per <= 512 * IPT) {  // one block; the pool fits it: no merge, no long path
+            if constexpr (S::kDT == kF64 && S::kC == 4) {
+                // one-member f64 tables (the hc select, amg_test.py:451-452): one load per
+                // item slot, not UNR copies of member 0 (measured 8.0 -> 7.3 us)
+                if (a.M == 1) {
+                    launch_tiles<S, S, IPT, 0, 512, 1, false, false>(src, src, ta, 1, q, oval, oidx, excl, st);
+                    launched = true;
+                    return;
+                }
+            }
             launch_tiles<S, S, IPT, 0, 512, small_unr<S, 512>(), false, false>(src, src, ta, 1, q, oval, oidx, excl,
                                                                                 st);
         } else if (per <= 1024 * IPT) {
