@@ -257,8 +257,10 @@ static inline StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx)
     s.ocand = nullptr;
     s.extra = nullptr;
     static const int ileave = [] {
+        // A/B knob CE_AMD_ILEAVE: 0 contiguous run per wave, 1 block-interleaved tiles,
+        // 2 grid-cyclic tiles; unset = the kernel's default per layout (-1)
         const char* e = getenv("CE_AMD_ILEAVE");
-        return (e && e[0] == '1') ? 1 : 0;
+        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
     }();
     s.ileave = ileave;
     return s;

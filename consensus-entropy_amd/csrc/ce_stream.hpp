@@ -366,7 +366,7 @@ struct StreamArgs {
     int64_t per_wave;  // items per wave (multiple of 64)
     const uint32_t* excl;  // exclusion bitmap over items 0..N-1 (1 = out of the pool), or nullptr
     int nlists;        // workspace lists (>= gridDim.x); lists past the grid are written empty
-    int ileave;        // k_stream_nmc: the block's waves interleave 64-item tiles (A/B knob CE_AMD_ILEAVE)
+    int ileave;        // k_stream_nmc tile order: -1 the layout's default, 0 runs, 1 block-interleaved, 2 grid-cyclic
     // stage 2 folded in (ctr != nullptr): the last block merges the grid's
     // lists into (oval, oidx), or into q records at ocand
     uint32_t* ctr;
@@ -738,7 +738,19 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int64_t lo, hi, step;
-    if (a.ileave) {  // the block's 4 waves take alternate tiles of the block's run (adjacent bursts per member row)
+    // tile distribution (measured on two boxes, alternating runs,
+    // profiles/r03_tile_order.json): item-major -- grid-cyclic, equal on a box
+    // where contiguous runs reach 0.871 and +2.5 % (0.836 -> 0.859) on one where
+    // they reach only 0.836; member-major -- block-interleaved (+0.3-0.5 %),
+    // grid-cyclic 4 % slower there
+    const int mode = a.ileave >= 0 ? a.ileave : (MNC ? 1 : 2);
+    if (mode == 2) {  // grid-cyclic: wave g takes tiles g, g + W, g + 2W, ... (W = the grid's waves), so
+        // the tiles in flight at any moment form one contiguous sweep of the pool
+        const int64_t W = (int64_t)gridDim.x * 4;
+        lo = ((int64_t)blockIdx.x * 4 + w) * 64;
+        hi = a.N;
+        step = W * 64;
+    } else if (mode == 1) {  // the block's 4 waves take alternate tiles of the block's run (adjacent bursts per member row)
         const int64_t blo = (int64_t)blockIdx.x * 4 * a.per_wave;
         hi = blo + 4 * a.per_wave < a.N ? blo + 4 * a.per_wave : a.N;
         lo = blo + 64 * w;
