@@ -368,10 +368,26 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
     double* row = wsm + w * wide_lds_doubles(a.C);
     double* scratch = row + a.C;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
-    int64_t lo = gw * sa.per_wave;
-    int64_t hi = lo + sa.per_wave;
-    if (hi > a.N) hi = a.N;
-    if (lo > hi) lo = hi;
+    // the wave's items: cnt items lo0, lo0 + stride, ...  -- grid-cyclic by
+    // default (wave g takes items g, g + W, ...: the items in flight at any
+    // moment are one contiguous sweep; C5 job 0.754-0.770 -> 0.779-0.781 of
+    // HBM on one box, profiles/r03_tile_order.json) or a contiguous run per
+    // wave (CE_AMD_ILEAVE=0 / 1)
+    int64_t lo0, stride, cnt;
+    if (sa.ileave < 0 || sa.ileave == 2) {
+        const int64_t W = (int64_t)gridDim.x * 4;
+        lo0 = gw;
+        stride = W;
+        cnt = a.N > gw ? (a.N - gw + W - 1) / W : 0;
+    } else {
+        int64_t lo = gw * sa.per_wave;
+        int64_t hi = lo + sa.per_wave;
+        if (hi > a.N) hi = a.N;
+        if (lo > hi) lo = hi;
+        lo0 = lo;
+        stride = 1;
+        cnt = hi - lo;
+    }
     RegTopQ tq;
     tq.init(q);
     const char* base = static_cast<const char*>(a.p);
@@ -382,8 +398,9 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
 #pragma unroll
     for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
     uint64_t mykey = 0;
-    // issue cursor (item, batch) and consume cursor
-    int64_t ii = lo, ci = lo;
+    int64_t myidx = 0;
+    // issue cursor (item ordinal, batch) and consume cursor
+    int64_t ii = 0, ci = 0;
     int ib = 0, cb = 0;
     uint32_t off[KCH];  // this lane's chunk offsets in a member row (clamped into the row)
 #pragma unroll
@@ -393,7 +410,7 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
     }
     WideBatch<DT, KCH, UNR> buf[NB];  // ring: NB - 1 batches in flight while one is added
     auto issue = [&](WideBatch<DT, KCH, UNR>& X) {
-        X.issue(base + ii * sNb, ib * UNR, sMb, off);
+        X.issue(base + (lo0 + ii * stride) * sNb, ib * UNR, sMb, off);
         if (++ib == NBM) {
             ib = 0;
             ++ii;
@@ -410,13 +427,15 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
 #endif
 #pragma unroll
             for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
-            const int j = (int)((ci - lo) & 63);
-            if (lane == j) mykey = order_key(h);
-            if (j == 63 || ci == hi - 1) {
-                const int64_t t0 = ci - j;
+            const int j = (int)(ci & 63);
+            if (lane == j) {
+                mykey = order_key(h);
+                myidx = lo0 + ci * stride;
+            }
+            if (j == 63 || ci == cnt - 1) {
                 bool ok = lane <= j;
-                if (sa.excl) ok = ok && !excluded(sa.excl, t0 + (lane <= j ? lane : j));
-                tq.offer(mykey, t0 + lane + sa.base_idx, ok);
+                if (sa.excl) ok = ok && !excluded(sa.excl, lane <= j ? myidx : lo0 + ci * stride);
+                tq.offer(mykey, myidx + sa.base_idx, ok);
                 mykey = 0;
             }
             ++ci;
@@ -424,13 +443,13 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
     };
 #pragma unroll
     for (int b = 0; b < NB - 1; ++b)
-        if (ii < hi) issue(buf[b]);
-    while (ci < hi) {
+        if (ii < cnt) issue(buf[b]);
+    while (ci < cnt) {
 #pragma unroll
         for (int s = 0; s < NB; ++s) {  // compile-time ring slots: no register-array indexing
-            if (ii < hi) issue(buf[(s + NB - 1) % NB]);
+            if (ii < cnt) issue(buf[(s + NB - 1) % NB]);
             consume(buf[s]);
-            if (ci >= hi) break;
+            if (ci >= cnt) break;
         }
     }
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists, nullptr, nullptr, 4, sa.ctr != nullptr);
