@@ -38,6 +38,11 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     fa.invM = 1.0 / (double)M;
     fa.pow2 = (M & (M - 1)) == 0;
     fa.base_idx = base_idx;
+    static const int order = [] {
+        const char* e = getenv("CE_AMD_ILEAVE");
+        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+    }();
+    fa.order = order;
     fa.nlists = G;
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, G, q);
