@@ -356,7 +356,10 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 #else
 #define CE_WIDE2_WPE
 #endif
-template <int DT, int KCH, int UNR, int NB = 2>
+#ifndef CE_WIDE2_NB
+#define CE_WIDE2_NB 2  // register ring depth (A/B builds: -DCE_WIDE2_NB=3)
+#endif
+template <int DT, int KCH, int UNR, int NB = CE_WIDE2_NB>
 __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
@@ -483,10 +486,21 @@ __global__ __launch_bounds__(kBS) void k_stream_wide_dma(WideArgs a, PwPlan pl, 
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     char* buf = wbuf + w * bufb;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
-    int64_t lo = gw * sa.per_wave;
-    int64_t hi = lo + sa.per_wave;
-    if (hi > a.N) hi = a.N;
-    if (lo > hi) lo = hi;
+    int64_t lo0, stride, cnt;  // the wave's items lo0 + k * stride, k < cnt (grid-cyclic by default)
+    if (sa.ileave < 0 || sa.ileave == 2) {
+        const int64_t W = (int64_t)gridDim.x * 4;
+        lo0 = gw;
+        stride = W;
+        cnt = a.N > gw ? (a.N - gw + W - 1) / W : 0;
+    } else {
+        int64_t lo = gw * sa.per_wave;
+        int64_t hi = lo + sa.per_wave;
+        if (hi > a.N) hi = a.N;
+        if (lo > hi) lo = hi;
+        lo0 = lo;
+        stride = 1;
+        cnt = hi - lo;
+    }
     RegTopQ tq;
     tq.init(q);
     const char* base = static_cast<const char*>(a.p);
@@ -518,8 +532,10 @@ __global__ __launch_bounds__(kBS) void k_stream_wide_dma(WideArgs a, PwPlan pl, 
 #pragma unroll
     for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
     uint64_t mykey = 0;
-    if (lo < hi) issue_tile(lo, 0);
-    for (int64_t it = lo; it < hi; ++it) {
+    int64_t myidx = 0;
+    if (cnt > 0) issue_tile(lo0, 0);
+    for (int64_t kx = 0; kx < cnt; ++kx) {
+        const int64_t it = lo0 + kx * stride;
         for (int k = 0; k < NT; ++k) {
             const int rows = a.M - k * T < T ? a.M - k * T : T;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -552,14 +568,16 @@ __global__ __launch_bounds__(kBS) void k_stream_wide_dma(WideArgs a, PwPlan pl, 
 #pragma unroll
         for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
         __builtin_amdgcn_sched_barrier(0);
-        if (it + 1 < hi) issue_tile(it + 1, 0);
-        const int j = (int)((it - lo) & 63);
-        if (lane == j) mykey = order_key(h);
-        if (j == 63 || it == hi - 1) {
-            const int64_t t0 = it - j;
+        if (kx + 1 < cnt) issue_tile(it + stride, 0);
+        const int j = (int)(kx & 63);
+        if (lane == j) {
+            mykey = order_key(h);
+            myidx = it;
+        }
+        if (j == 63 || kx == cnt - 1) {
             bool ok = lane <= j;
-            if (sa.excl) ok = ok && !excluded(sa.excl, t0 + (lane <= j ? lane : j));
-            tq.offer(mykey, t0 + lane + sa.base_idx, ok);
+            if (sa.excl) ok = ok && !excluded(sa.excl, lane <= j ? myidx : it);
+            tq.offer(mykey, myidx + sa.base_idx, ok);
             mykey = 0;
         }
     }
