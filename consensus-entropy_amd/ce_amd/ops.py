@@ -40,16 +40,29 @@ def new_workspace(nbytes, device):
 
 
 class _WorkspaceCache:
-    """Per-device scratch reused across calls (grows, never shrinks), so steady
-    state allocates nothing."""
+    """Scratch reused across calls, one per (device, stream): include/ce.h
+    allows one workspace per stream -- its header holds the arrival counters of
+    the folded merges, so two streams sharing one would mix their tickets.  A
+    buffer grows (never shrinks), so steady state allocates nothing.
+
+    Under HIP-graph capture every call gets a FRESH zero-filled workspace
+    allocated inside the capture (from the graph's private pool; its zero fill
+    is a captured memset that runs at every replay): a graph never references a
+    cached buffer, so growing the cache later cannot free memory a graph still
+    uses, and replays never share counters with eager calls."""
 
     def __init__(self):
         self._ws = {}
 
     def get(self, device, nbytes):
-        key = torch.device(device).index
+        device = torch.device(device)
+        if torch.cuda.is_current_stream_capturing():
+            return new_workspace(nbytes, device)
+        key = (device.index, torch.cuda.current_stream(device).cuda_stream)
         buf = self._ws.get(key)
         if buf is None or buf.numel() < nbytes:
+            # the old buffer (if any) is released on this stream: the caching
+            # allocator reuses its block only in this stream's order
             buf = new_workspace(nbytes, device)
             self._ws[key] = buf
         return buf
@@ -200,15 +213,26 @@ def select_frames(members, offsets, q, perm=None, base_idx=0, song_level=None):
         perm = perm.to(torch.int64).contiguous()
     q = _check_q(q)
     C = members[0].shape[1]
-    arr = (_Member * len(members))()
-    keep = []
-    F = perm.numel() if perm is not None else None
-    if F is None:  # a member with other than N rows holds the frames: F without a device read
-        F = next((t.shape[0] for t in members if t.dim() == 2 and t.shape[0] != N), None)
     for m, t in enumerate(members):
         _on_gpu(t, f"member {m}")
         if t.dim() != 2 or t.shape[1] != C or t.dtype not in (torch.float32, torch.float64):
             raise ValueError(f"member {m} must be a float32/float64 [*, {C}] tensor")
+    if song_level is not None and len(song_level) != len(members):
+        raise ValueError("song_level needs one flag per member")
+    # F (frames): the permutation's length, else the row count of the frame-level
+    # members (rows other than N, or flagged frame-level), else one device read
+    F = perm.numel() if perm is not None else None
+    if F is None:
+        fr = {t.shape[0] for m, t in enumerate(members)
+              if (not bool(song_level[m]) if song_level is not None else t.shape[0] != N)}
+        if len(fr) > 1:
+            raise ValueError(f"frame-level members disagree on the frame count: {sorted(fr)}")
+        F = fr.pop() if fr else None
+    if F is None:  # every member has N rows: only the offsets tell
+        F = int(offsets[-1])
+    arr = (_Member * len(members))()
+    keep = []
+    for m, t in enumerate(members):
         if t.stride(1) != 1:
             t = t.contiguous()
         keep.append(t)
@@ -217,9 +241,12 @@ def select_frames(members, offsets, q, perm=None, base_idx=0, song_level=None):
         elif t.shape[0] != N:
             sl = False
         else:  # N rows: song-level unless there are exactly N frames too
-            if F is None:  # every member has N rows: only the offsets tell (one device read)
-                F = int(offsets[-1])
             sl = F != N
+        # the kernel reads row n of a song-level member and rows < F of a frame-level one
+        need = N if sl else F
+        if t.shape[0] < need:
+            raise ValueError(f"member {m} has {t.shape[0]} rows; a {'song' if sl else 'frame'}-level member needs "
+                             f">= {need}")
         arr[m] = _Member(t.data_ptr(), _DT[t.dtype], 1 if sl else 0, t.stride(0))
     lib = _lib.load()
     ws = WORKSPACE.get(offsets.device, lib.ce_select_frames_workspace_bytes(N, q))

@@ -24,11 +24,11 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     if (!ws || ws_bytes < lists_bytes((int64_t)G1 + G2, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, (int64_t)G1 + G2, q);
-    if (small_enabled() && q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= kSmallPoolItems && N_h <= kSmallPoolItems &&
+    if (q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= kSmallPoolItems && N_h <= kSmallPoolItems &&
         C == 4) {
         // both segments in ONE launch: tiles of either segment, ticketed merge (k_select_tiles)
         const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
-        if (launch_small_mix(a, t, q, val_out, idx_out, w, st)) return check_launch("ce_select_mix");
+        if (launch_small_mix(a, t, q, val_out, idx_out, st)) return check_launch("ce_select_mix");
     }
     // both segments on the streaming engine when it applies (q <= 64): the hc
     // table is a committee of M = 1 member ([N_h, 1, C] f64, row stride ld_hc)
@@ -64,9 +64,10 @@ static int batched_bpu(int64_t total, int U) {
     return (int)bpu;
 }
 
-// lists of either batched path: bpu per user (k_stream_seg) or the tiles (k_select_tiles)
+// lists of the k_stream_seg path: bpu per user (k_select_tiles writes none)
 static int64_t batched_lists(int64_t total_items, int U, int q) {
-    return (int64_t)std::max(batched_bpu(total_items, U), small_users_tiles(total_items, U, q)) * U;
+    (void)q;
+    return (int64_t)batched_bpu(total_items, U) * U;
 }
 
 extern "C" size_t ce_select_batched_workspace_bytes(int64_t total_items, int32_t U, int32_t q) {
@@ -90,12 +91,11 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
         return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, nl, q);
-    if (small_enabled() && q <= kStreamMaxQ) {
-        // each user over a few tiles, ticketed per-user merge (k_select_tiles; a
-        // user longer than its tiles streams inside them)
-        if (launch_small_users(a, offsets, U, q, val_out, idx_out, w, st)) return check_launch("ce_select_batched");
+    if (q <= kStreamMaxQ) {
+        // one block per user (k_select_tiles; a user longer than its block streams inside it)
+        if (launch_small_users(a, offsets, U, q, val_out, idx_out, st)) return check_launch("ce_select_batched");
     }
-    if (stream_enabled() && q <= kStreamMaxQ) {
+    if (q <= kStreamMaxQ) {
         // bpu 4-wave blocks per user, then one wave per user merges its bpu lists
         if (launch_seg(a, offsets, 0, 0, q, (int)nl, bpu, bpu == 1 && U < 64 ? 64 * kSegWaves : 256, val_out, idx_out,
                        w.c, nullptr, st)) {

@@ -13,19 +13,15 @@ __global__ __launch_bounds__(kBS) void k_log(const double* __restrict__ x, int64
 }
 
 // x[i] / s[i] through the entropy path's shared-reciprocal division
-// (RowDivisor, ce_device.hpp) -- verification against IEEE division.
+// (row_quotients, ce_device.hpp) -- verification against IEEE division.
 __global__ __launch_bounds__(kBS) void k_rowdiv(const double* __restrict__ x, const double* __restrict__ s, int64_t n,
                                                 double* __restrict__ y) {
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS)
     {
-#ifdef CE_ROWDIV
         const double xi[1] = {x[i]};  // the row-level range test of the entropy kernels, one class per row
         double d[1];
         row_quotients<1>(xi, s[i], d);
         y[i] = d[0];
-#else
-        y[i] = RowDivisor(s[i]).div(x[i]);
-#endif
     }
 }
 
@@ -197,25 +193,6 @@ static int with_nx(int D, F&& f) {
     return CE_EUNSUPPORTED;
 }
 
-// A/B knob: CE_AMD_GNB_STREAM=0 -> k_gnb_proba8 for the reference's shape too
-static bool gnb_stream_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_GNB_STREAM");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// A/B knob: CE_AMD_GNB_WPE = 2 / 3 / 4 waves per SIMD for k_gnb_stream260 (register cap; 3 = 166 VGPRs,
-// no spills, measured fastest: 2.48 ms at 4M frames vs 2.69 ms for 4 waves with spills)
-static int gnb_waves_per_simd() {
-    static const int v = [] {
-        const char* e = getenv("CE_AMD_GNB_WPE");
-        return (e && e[0] >= '2' && e[0] <= '4') ? e[0] - '0' : 3;
-    }();
-    return v;
-}
-
 // >= ~8 eight-frame passes per wave, so each block's LDS staging is amortised
 static int member_grid8(int64_t F) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(F, 256), 2048)); }
 
@@ -232,9 +209,10 @@ extern "C" int ce_gnb_predict_proba(const double* X, int64_t F, int32_t D, int64
     GnbArgs a{X, F, D, ld, theta, var, log_prior, C, out, ld_out};
     const PwPlan pl = pw_plan(D);
     const size_t lds = (size_t)3 * C * D * sizeof(double);  // up to 96 KB at C = 8, D = 512
-    if (D == 260 && ld == 260 && C == 4 && gnb_stream_enabled()) {  // the reference's contiguous rows: feature-streamed
-        const int wpe = gnb_waves_per_simd();
-        auto kern = wpe == 2 ? k_gnb_stream260<4, 2> : (wpe == 4 ? k_gnb_stream260<4, 4> : k_gnb_stream260<4, 3>);
+    if (D == 260 && ld == 260 && C == 4) {  // the reference's contiguous rows: feature-streamed
+        // 3 waves per SIMD (166 VGPRs, no spills) measured fastest: 2.48 ms at 4M
+        // frames vs 2.69 ms for 4 waves with spills
+        auto kern = k_gnb_stream260<4, 3>;
         const int grid = resident_grid(kern, 0, (int)std::min<int64_t>(cdiv(F, 32), 1 << 20));
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
         return check_launch("ce_gnb_predict_proba");

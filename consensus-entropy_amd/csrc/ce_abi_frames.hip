@@ -38,11 +38,6 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     fa.invM = 1.0 / (double)M;
     fa.pow2 = (M & (M - 1)) == 0;
     fa.base_idx = base_idx;
-    static const int order = [] {
-        const char* e = getenv("CE_AMD_ILEAVE");
-        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
-    }();
-    fa.order = order;
     fa.nlists = G;
     hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, G, q);
@@ -57,11 +52,9 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     };
     // C lanes per song (k_frames_lanes: whole-row reads, LDS-DMA tiles for
     // grouped dense members) where C divides the wave; lane per song otherwise
-    static const bool lanes = [] {  // A/B knob: CE_AMD_FRAMES_LANES=0 -> k_frames_select
-        const char* e = getenv("CE_AMD_FRAMES_LANES");
-        return !(e && e[0] == '0');
-    }();
-    static const int dma_env = [] {  // A/B knob: CE_AMD_FRAMES_DMA=0 / 1 forces direct loads / LDS-DMA tiles
+    // (k_frames_select, measured 2.7x slower at 1M songs x 40 frames)
+    static const int dma_env = [] {  // test knob: CE_AMD_FRAMES_DMA=0 / 1 forces direct loads / LDS-DMA tiles
+        // (test_frames_dma_tiles_vs_oracle runs the tiles at the oracle's sizes with it)
         const char* e = getenv("CE_AMD_FRAMES_DMA");
         return e ? (e[0] == '0' ? 0 : 1) : -1;
     }();
@@ -76,10 +69,10 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
         else go(direct_kern, step);
     };
     switch (C) {
-        case 2: lanes ? lanes_go(k_frames_lanes<2, true>, k_frames_lanes<2, false>, 32) : go(k_frames_select<2>, 64); break;
+        case 2: lanes_go(k_frames_lanes<2, true>, k_frames_lanes<2, false>, 32); break;
         case 3: go(k_frames_select<3>, 64); break;
-        case 4: lanes ? lanes_go(k_frames_lanes<4, true>, k_frames_lanes<4, false>, 16) : go(k_frames_select<4>, 64); break;
-        default: lanes ? lanes_go(k_frames_lanes<8, true>, k_frames_lanes<8, false>, 8) : go(k_frames_select<8>, 64); break;
+        case 4: lanes_go(k_frames_lanes<4, true>, k_frames_lanes<4, false>, 16); break;
+        default: lanes_go(k_frames_lanes<8, true>, k_frames_lanes<8, false>, 8); break;
     }
     return check_launch("ce_select_frames");
 }

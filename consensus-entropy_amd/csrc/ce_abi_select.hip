@@ -60,12 +60,12 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
     if (rc0) return rc0;
     // the workspace contract holds on every path, even the one that does not touch it
     if (!ws || ws_bytes < lists_bytes(pool_blocks(N), q)) return fail(CE_EWORKSPACE, "workspace too small");
-    if (small_enabled() && q <= kStreamMaxQ && N > 0) {
+    if (q <= kStreamMaxQ && N > 0) {
         // the pool over a few tiles, ticketed merge, one launch (k_select_tiles)
         if (launch_small_pool(a, base_idx, q, val_out, idx_out, excl, carve(ws, 0, q), st))
             return check_launch("ce_select_mc");
     }
-    if (stream_enabled() && q <= kStreamMaxQ && N > 0 &&
+    if (q <= kStreamMaxQ && N > 0 &&
         N * (int64_t)M * C * elem_bytes((int)dt) <= kSmallPoolBytes) {
         // small pool: ~512 items per 4-wave block on a few CUs (one block: it
         // is the final answer), then one wave merges the blocks' lists

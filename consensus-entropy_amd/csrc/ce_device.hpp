@@ -95,67 +95,23 @@ __device__ __forceinline__ double row_sum(const double (&a)[C]) {
     return 0.0 + pairwise<0, C, C>(a);
 }
 
-// ---------------------------------------------------------------------------
-// x / s for many x and one s, bit-identical to separate IEEE divisions.
-// gfx950's f64 division (LLVM's lowering; see DESIGN.md "Numerics") is
-//   d = v_div_scale(s), n = v_div_scale(x); r = v_rcp_f64(d), two Newton steps
-//   r = fma(r, fma(-d, r, 1), r); q = n * r; rem = fma(-d, q, n);
-//   v_div_fmas(rem, r, q) = fma(rem, r, q) (+ rescale); v_div_fixup (specials)
-// When neither operand needs scaling -- both in [2^-300, 2^300), or x == 0 --
-// the scale steps return their input, v_div_fmas is a plain fma and
-// v_div_fixup returns its input, so r depends on s alone: the row's C
-// quotients cost 5 + 3C instructions instead of ~11C.  Anything else (zero,
-// tiny, huge, inf, NaN) takes the ordinary division; a zero numerator returns
-// x * r, whose sign is IEEE's (the first device test caught -0 / s giving +0
-// through the correction step).  Opt-in (-DCE_FASTDIV, the A/B build `make
-// fastdiv`) until the device test holds it bit-exact.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ bool div_plain_range(double x) {  // exponent field in [1023-300, 1023+300)
-    return ((((uint32_t)(dbits(x) >> 32)) >> 20) & 0x7ffu) - 723u < 600u;
-}
-struct RowDivisor {
-    double s, r;
-    bool fast;
-    __device__ __forceinline__ explicit RowDivisor(double s_) : s(s_), r(0.0), fast(div_plain_range(s_)) {
-#ifdef CE_FASTDIV
-        if (fast) {
-            double r0 = __builtin_amdgcn_rcp(s);
-            r0 = __builtin_fma(r0, __builtin_fma(-s, r0, 1.0), r0);
-            r = __builtin_fma(r0, __builtin_fma(-s, r0, 1.0), r0);
-        }
-#endif
-    }
-    __device__ __forceinline__ double div(double x) const {
-#ifdef CE_FASTDIV
-        const bool zero = x == 0.0;
-        if (fast && (zero || div_plain_range(x))) {
-            const double q = x * r;  // a zero numerator: +-0 with IEEE's sign (the correction would give +0)
-            const double res = __builtin_fma(__builtin_fma(-s, q, x), r, q);
-            return zero ? q : res;
-        }
-#endif
-        return x / s;
-    }
-};
-
-// The row's C quotients x[c] / s with ONE range test for the whole row
-// (-DCE_ROWDIV): when every x[c] and s is positive with its exponent field in
-// [723, 1323) -- [2^-300, 2^300) -- both v_div_scale steps return their
-// inputs (no operand is zero, tiny or huge, quotient exponents differ by
-// < 768), v_div_fmas is a plain fma and v_div_fixup returns its input, so
-// x / s == fma(fma(-s, q, x), r, q), q = x * r, with r the division's own
-// refined reciprocal of s: one reciprocal per row, 3 instructions per class
-// instead of ~11.  Rows with a zero, a tiny or a negative value (and NaN /
-// inf) take the ordinary divisions.  The range test is two min/max folds of
-// the high words and one compare.
-// on by default (measured: C3 14.24 -> 13.36 us with the throttled slots, the
-// C4 stream unchanged); -DCE_NO_ROWDIV builds the plain divisions for A/B
-#if !defined(CE_NO_ROWDIV) && !defined(CE_ROWDIV)
-#define CE_ROWDIV 1
-#endif
+// The row's C quotients x[c] / s, bit-identical to C separate IEEE
+// divisions, with ONE reciprocal per row.  gfx950's f64 division (LLVM's
+// lowering) is d = v_div_scale(s), n = v_div_scale(x); r = v_rcp_f64(d), two
+// Newton steps r = fma(r, fma(-d, r, 1), r); q = n * r; rem = fma(-d, q, n);
+// v_div_fmas(rem, r, q) = fma(rem, r, q) (+ rescale); v_div_fixup (specials).
+// When every x[c] and s is positive with its exponent field in [723, 1323) --
+// [2^-300, 2^300) -- both v_div_scale steps return their inputs (no operand is
+// zero, tiny or huge, quotient exponents differ by < 768), v_div_fmas is a
+// plain fma and v_div_fixup returns its input, so x / s == fma(fma(-s, q, x),
+// r, q), q = x * r, with r the division's own refined reciprocal of s:
+// 3 instructions per class instead of ~11.  Rows with a zero, a tiny or a
+// negative value (and NaN / inf) take the ordinary divisions.  The range test
+// is two min/max folds of the high words and one compare.  Measured: C3
+// 14.24 -> 13.36 us, the C4 stream unchanged; held bit-exact by
+// test_row_division_bit_exact (6e7 pairs across and beyond the range).
 template <int C>
 __device__ __forceinline__ void row_quotients(const double (&x)[C], double s, double (&d)[C]) {
-#ifdef CE_ROWDIV
     const uint32_t hs = (uint32_t)(dbits(s) >> 32);
     uint32_t lo = hs, hi = hs;
 #pragma unroll
@@ -175,7 +131,6 @@ __device__ __forceinline__ void row_quotients(const double (&x)[C], double s, do
         }
         return;
     }
-#endif
 #pragma unroll
     for (int c = 0; c < C; ++c) d[c] = x[c] / s;
 }
@@ -185,7 +140,6 @@ template <int C>
 __device__ __forceinline__ double entropy_row(const double (&mean)[C]) {
     const double s = row_sum<C>(mean);
     double e[C];
-#if defined(CE_ROWDIV)
     if constexpr (C <= 8) {
         double d[C];
         row_quotients<C>(mean, s, d);
@@ -193,10 +147,8 @@ __device__ __forceinline__ double entropy_row(const double (&mean)[C]) {
         for (int c = 0; c < C; ++c) e[c] = entr(d[c]);
         return row_sum<C>(e);
     }
-#endif
-    const RowDivisor d(s);
 #pragma unroll
-    for (int c = 0; c < C; ++c) e[c] = entr(d.div(1.0 * mean[c]));
+    for (int c = 0; c < C; ++c) e[c] = entr(1.0 * mean[c] / s);
     return row_sum<C>(e);
 }
 

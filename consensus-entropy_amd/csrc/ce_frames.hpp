@@ -43,7 +43,6 @@ struct FrameArgs {
     bool pow2;
     int64_t base_idx;
     int64_t per_wave;  // songs per wave (a multiple of the kernel's songs per wave step)
-    int order;         // k_frames_lanes: -1 / 2 grid-cyclic steps, 0 / 1 a run per wave (CE_AMD_ILEAVE)
     int nlists;
     uint32_t* ctr;  // fold (last block merges the grid)
     double* oval;
@@ -199,18 +198,8 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
     const int sg = lane / C, c = lane - sg * C;
     char* tile = tiles[w];
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
-    int64_t lo, hi, step;
-    if (a.order < 0 || a.order == 2) {  // grid-cyclic steps (wave g: steps g, g + W, ...)
-        lo = gw * G;
-        hi = a.N;
-        step = (int64_t)gridDim.x * 4 * G;
-    } else {  // a contiguous run of songs per wave
-        lo = gw * a.per_wave;
-        hi = lo + a.per_wave;
-        if (hi > a.N) hi = a.N;
-        if (lo > hi) lo = hi;
-        step = G;
-    }
+    // grid-cyclic steps (wave g: steps g, g + W, ...; ~1 % over a contiguous run per wave)
+    const int64_t lo = gw * G, hi = a.N, step = (int64_t)gridDim.x * 4 * G;
     RegTopQ tq;
     tq.init(q);
     for (int64_t t0 = lo; t0 < hi; t0 += step) {

@@ -162,56 +162,6 @@ static inline int with_wide_v(const CommArgs& a, F&& f) {
 }
 
 // ---- streaming stage 1 (q <= 64): wave-independent, LDS-DMA for item-major ----
-static inline bool stream_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_STREAM");  // A/B knob: CE_AMD_STREAM=0 -> block-synchronous k_partial
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// Cache policy of the item-major LDS-DMA stream: nt (default) or the default
-// policy (A/B knob CE_AMD_DMA_NT=0).
-static inline bool dma_nt() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_DMA_NT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// A/B knob: CE_AMD_WIDE2=0 -> the unpipelined wide kernel (k_stream_wide)
-// A/B knob: CE_AMD_WIDE_DMA=1 -> the LDS-DMA tile stream (k_stream_wide_dma)
-// instead of the register-ring wide stream (k_stream_wide2).  Off by default:
-// on the C5 job (12M items, 2M-item chunks, one box, alternating runs) it
-// measured 0.760 / 0.752 of HBM against 0.773 / 0.772 -- 16 KiB in flight per
-// wave (128 KiB per CU, 2.7x the register ring's) bought nothing, so the wide
-// stream is not limited by the bytes it keeps in flight
-static inline bool wide_dma_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_WIDE_DMA");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
-static inline bool wide2_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_WIDE2");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-static inline bool small_enabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("CE_AMD_SMALL");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
-
 // Blocks of `kernel` resident on the whole device (occupancy API x CUs), cached.
 static inline int device_cus() {
     static int cus[64] = {0};
@@ -256,13 +206,6 @@ static inline StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx)
     s.oidx = nullptr;
     s.ocand = nullptr;
     s.extra = nullptr;
-    static const int ileave = [] {
-        // A/B knob CE_AMD_ILEAVE: 0 contiguous run per wave, 1 block-interleaved tiles,
-        // 2 grid-cyclic tiles; unset = the kernel's default per layout (-1)
-        const char* e = getenv("CE_AMD_ILEAVE");
-        return (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
-    }();
-    s.ileave = ileave;
     return s;
 }
 
@@ -315,20 +258,18 @@ CE_HIDDEN void launch_finish_vals(const double* vals, const int64_t* idx, int se
                                   double* oval, int64_t* oidx, hipStream_t st);
 CE_HIDDEN void launch_merge_wave(const Cand* c, int segs, int nl, int q, double* oval, int64_t* oidx,
                                  hipStream_t st);
-// ce_launch_small.hip: pools of a few thousand items, tiled over blocks with
-// an arrival-ticket merge (k_select_tiles, ce_small.hpp).
-constexpr int kTileBS = 256;
+// ce_launch_small.hip: pools of a few thousand items, one block per problem
+// (k_select_tiles, ce_small.hpp).
 // one pool of a.N items (<= kSmallPoolItems); false: too large / no kernel
 constexpr int64_t kSmallPoolItems = 4096;
 CE_HIDDEN bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval, int64_t* oidx,
                                  const uint32_t* excl, WsLists w, hipStream_t st);
-// U users (offsets[U+1]) in one launch, small_users_tiles() tiles per user
-CE_HIDDEN int small_users_tiles(int64_t total_items, int U, int q);
+// U users (offsets[U+1]) in one launch, one block per user
 CE_HIDDEN bool launch_small_users(const CommArgs& a, const int64_t* offsets, int U, int q, double* oval,
-                                  int64_t* oidx, WsLists w, hipStream_t st);
-// the mix of amg_test.py:473-480 ([mc; hc] rows, C = 4 or 8) in one launch
+                                  int64_t* oidx, hipStream_t st);
+// the mix of amg_test.py:473-480 ([mc; hc] rows, C = 4) in one launch
 CE_HIDDEN bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, double* oval, int64_t* oidx,
-                                WsLists w, hipStream_t st);
+                                hipStream_t st);
 // k_stream_seg over `nblocks` blocks of `threads` (bpu blocks per segment)
 CE_HIDDEN bool launch_seg(const CommArgs& a, const int64_t* offsets, int64_t n, int64_t base_idx, int q, int nblocks,
                           int bpu, int threads, double* oval, int64_t* oidx, Cand* wc, const uint32_t* excl,

@@ -47,14 +47,10 @@ struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
 
-// item slots a lane keeps in flight in the single-block pools (keys_small);
-// 0 = all of them at once.  Measured on configs[2] (500 users x 1608, f32):
-// all at once 14.24 us, 1 slot 13.52 us, 2 slots 14.68 us (A/B builds:
-// -DCE_SMALL_THR=0/2)
-#ifndef CE_SMALL_THR
-#define CE_SMALL_THR 1
-#endif
-constexpr int kSmallThrottle = CE_SMALL_THR;
+// item slots a lane keeps in flight in the single-block pools (keys_small).
+// Measured on configs[2] (500 users x 1608, f32): all at once 14.24 us,
+// 1 slot 13.52 us, 2 slots 14.68 us
+constexpr int kSmallThrottle = 1;
 
 template <int DT, int C, bool VEC>
 struct CommitteeSrc {
@@ -348,19 +344,11 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 // has 2 x UNR x KCH 16-B loads per lane outstanding.  Items per wave are not
 // rounded to 64 (a wide item is tens of KB): every wave of the resident grid
 // gets work.
-// A/B builds (make wide_ab): -DCE_WIDE2_WPE4 caps the wide stream at 128
-// VGPRs (4 waves per SIMD); -DCE_WIDE_ENTR_LDS feeds its entr pass from the
-// LDS row (wave_entropy_from_sums_lds: fewer live registers in that phase).
-#ifdef CE_WIDE2_WPE4
-#define CE_WIDE2_WPE __attribute__((amdgpu_waves_per_eu(4)))
-#else
-#define CE_WIDE2_WPE
-#endif
-#ifndef CE_WIDE2_NB
-#define CE_WIDE2_NB 2  // register ring depth (A/B builds: -DCE_WIDE2_NB=3)
-#endif
-template <int DT, int KCH, int UNR, int NB = CE_WIDE2_NB>
-__global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
+// Measured and not kept: a 3-deep ring (0.782-0.784 vs
+// 0.790-0.801 of HBM), a 4-wave register cap, the entr pass fed from the LDS
+// row, and 16 KiB LDS-DMA tiles per wave (1.5-2.5 % slower on the C5 job).
+template <int DT, int KCH, int UNR, int NB = 2>
+__global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     CE_DASSERT((int)gridDim.x <= sa.nlists && q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
@@ -371,26 +359,13 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
     double* row = wsm + w * wide_lds_doubles(a.C);
     double* scratch = row + a.C;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
-    // the wave's items: cnt items lo0, lo0 + stride, ...  -- grid-cyclic by
-    // default (wave g takes items g, g + W, ...: the items in flight at any
-    // moment are one contiguous sweep; C5 job 0.754-0.770 -> 0.779-0.781 of
-    // HBM on one box, profiles/r03_tile_order.json) or a contiguous run per
-    // wave (CE_AMD_ILEAVE=0 / 1)
-    int64_t lo0, stride, cnt;
-    if (sa.ileave < 0 || sa.ileave == 2) {
-        const int64_t W = (int64_t)gridDim.x * 4;
-        lo0 = gw;
-        stride = W;
-        cnt = a.N > gw ? (a.N - gw + W - 1) / W : 0;
-    } else {
-        int64_t lo = gw * sa.per_wave;
-        int64_t hi = lo + sa.per_wave;
-        if (hi > a.N) hi = a.N;
-        if (lo > hi) lo = hi;
-        lo0 = lo;
-        stride = 1;
-        cnt = hi - lo;
-    }
+    // the wave's items: cnt items lo0, lo0 + stride, ...  -- grid-cyclic (wave
+    // g takes items g, g + W, ...: the items in flight at any moment are one
+    // contiguous sweep; C5 job 0.754-0.770 -> 0.779-0.781 of HBM against a
+    // contiguous run per wave on one box, profiles/r03_tile_order.json)
+    const int64_t W = (int64_t)gridDim.x * 4;
+    const int64_t lo0 = gw, stride = W;
+    const int64_t cnt = a.N > gw ? (a.N - gw + W - 1) / W : 0;
     RegTopQ tq;
     tq.init(q);
     const char* base = static_cast<const char*>(a.p);
@@ -423,11 +398,7 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
         X.add(acc);
         if (++cb == NBM) {  // item ci complete
             cb = 0;
-#ifdef CE_WIDE_ENTR_LDS
-            const double h = wave_entropy_from_sums_lds<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
-#else
             const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
-#endif
 #pragma unroll
             for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
             const int j = (int)(ci & 63);
@@ -453,132 +424,6 @@ __global__ __launch_bounds__(kBS) CE_WIDE2_WPE void k_stream_wide2(WideArgs a, P
             if (ii < cnt) issue(buf[(s + NB - 1) % NB]);
             consume(buf[s]);
             if (ci >= cnt) break;
-        }
-    }
-    block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists, nullptr, nullptr, 4, sa.ctr != nullptr);
-    if (sa.ctr) fold_merge<4>(sa.ctr, sa.oval, sa.oidx, sa.ocand, q, wc, sm, sa.extra);
-}
-
-// Wide classes by LDS-DMA (q <= 64): one wave per item as in k_stream_wide2,
-// but an item's member rows reach the wave as TILES of T contiguous rows
-// (T * C * size <= 16 KiB, rows of an item are contiguous: [N, M, C] with sM
-// == C) by global_load_lds_dwordx4, 1 KiB per instruction, into the wave's
-// own LDS buffer.  The wave waits for the tile, reads its 16-B chunks of the
-// T rows into registers, issues the NEXT tile's DMA into the same buffer and
-// only then adds the rows (member-sequential, as numpy's mean) -- so a whole
-// 16 KiB tile is in flight while the wave computes, without holding the bytes
-// in VGPRs (k_stream_wide2: 4 KiB per wave, 3 waves per SIMD).  Once an
-// item's last tile is read the buffer is free: it holds the mean row for the
-// two pairwise row sums of scipy.stats.entropy (wave_entropy_from_sums), then
-// the next item's first tile is issued.  bufb: bytes per wave buffer (>= the
-// tile and the padded row).  Lanes past a tile's last byte re-read its last
-// chunk (in bounds; they land past the tile in the buffer).
-template <int DT, int KCH, int AUX>
-__global__ __launch_bounds__(kBS) void k_stream_wide_dma(WideArgs a, PwPlan pl, StreamArgs sa, int q,
-                                                         Cand* __restrict__ wc, int T, int bufb) {
-    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
-    CE_DASSERT((int)gridDim.x <= sa.nlists && q >= 1 && q <= kStreamMaxQ && T >= 1);
-    __shared__ WaveLists sm;
-    extern __shared__ __attribute__((aligned(16))) char wbuf[];
-    constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
-    constexpr int TMAX = KCH >= 16 ? 1 : 16 / KCH;  // tile rows held in registers: 64 VGPRs of raw bytes
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    char* buf = wbuf + w * bufb;
-    const int64_t gw = (int64_t)blockIdx.x * 4 + w;
-    int64_t lo0, stride, cnt;  // the wave's items lo0 + k * stride, k < cnt (grid-cyclic by default)
-    if (sa.ileave < 0 || sa.ileave == 2) {
-        const int64_t W = (int64_t)gridDim.x * 4;
-        lo0 = gw;
-        stride = W;
-        cnt = a.N > gw ? (a.N - gw + W - 1) / W : 0;
-    } else {
-        int64_t lo = gw * sa.per_wave;
-        int64_t hi = lo + sa.per_wave;
-        if (hi > a.N) hi = a.N;
-        if (lo > hi) lo = hi;
-        lo0 = lo;
-        stride = 1;
-        cnt = hi - lo;
-    }
-    RegTopQ tq;
-    tq.init(q);
-    const char* base = static_cast<const char*>(a.p);
-    const int64_t sNb = a.sN * EB;
-    const int R = a.C * EB;  // bytes per member row
-    const int K = a.C / CPC;  // 16-B chunks per row
-    const int NT = (a.M + T - 1) / T;
-    CE_DASSERT(T <= TMAX && (int64_t)T * R <= bufb && K <= 64 * KCH);
-    uint32_t off[KCH];  // this lane's chunk offsets in a row (clamped into the row)
-#pragma unroll
-    for (int kk = 0; kk < KCH; ++kk) {
-        const int ch = lane + 64 * kk;
-        off[kk] = 16u * (uint32_t)(ch < K ? ch : K - 1);
-    }
-    auto issue_tile = [&](int64_t it, int k) {
-        const int r0 = k * T;
-        const int nb = (a.M - r0 < T ? a.M - r0 : T) * R;
-        const char* src0 = base + it * sNb + (int64_t)r0 * R;
-        const int nins = (nb + 1023) >> 10;
-        for (int j = 0; j < nins; ++j) {  // wave-uniform
-            int o = j * 1024 + lane * 16;
-            o = o < nb ? o : nb - 16;
-            CE_DASSERT(j * 1024 + 1024 <= bufb);
-            __builtin_amdgcn_global_load_lds((const void*)(src0 + o),
-                                             (void __attribute__((address_space(3)))*)(buf + j * 1024), 16, 0, AUX);
-        }
-    };
-    double acc[KCH * CPC];
-#pragma unroll
-    for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
-    uint64_t mykey = 0;
-    int64_t myidx = 0;
-    if (cnt > 0) issue_tile(lo0, 0);
-    for (int64_t kx = 0; kx < cnt; ++kx) {
-        const int64_t it = lo0 + kx * stride;
-        for (int k = 0; k < NT; ++k) {
-            const int rows = a.M - k * T < T ? a.M - k * T : T;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t v[TMAX][KCH][4];
-#pragma unroll
-            for (int r = 0; r < TMAX; ++r) {
-                if (r < rows) {  // wave-uniform
-#pragma unroll
-                    for (int kk = 0; kk < KCH; ++kk) {
-                        const u32x4 x = *reinterpret_cast<const u32x4*>(buf + r * R + off[kk]);
-                        v[r][kk][0] = x.x;
-                        v[r][kk][1] = x.y;
-                        v[r][kk][2] = x.z;
-                        v[r][kk][3] = x.w;
-                    }
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if (k + 1 < NT) issue_tile(it, k + 1);
-#pragma unroll
-            for (int r = 0; r < TMAX; ++r)
-                if (r < rows)
-#pragma unroll
-                    for (int kk = 0; kk < KCH; ++kk) chunk_add<DT>(v[r][kk], acc + kk * CPC);
-        }
-        // the buffer is free: the mean row and both row sums, then the next item's first tile
-        const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl,
-                                                         reinterpret_cast<double*>(buf), nullptr);
-#pragma unroll
-        for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
-        __builtin_amdgcn_sched_barrier(0);
-        if (kx + 1 < cnt) issue_tile(it + stride, 0);
-        const int j = (int)(kx & 63);
-        if (lane == j) {
-            mykey = order_key(h);
-            myidx = it;
-        }
-        if (j == 63 || kx == cnt - 1) {
-            bool ok = lane <= j;
-            if (sa.excl) ok = ok && !excluded(sa.excl, lane <= j ? myidx : it);
-            tq.offer(mykey, myidx + sa.base_idx, ok);
-            mykey = 0;
         }
     }
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists, nullptr, nullptr, 4, sa.ctr != nullptr);

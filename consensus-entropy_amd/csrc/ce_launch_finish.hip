@@ -6,21 +6,12 @@
 
 using namespace ce;
 
-// A/B knob: CE_AMD_MERGE_REG=0 -> the LDS-buffer merges (k_finish / k_finish_heads) for q <= 64 too
-static inline bool merge_reg_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_MERGE_REG");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 // ocand != nullptr: write candidate records (q <= kStreamMaxQ only) instead of (val, idx).
 template <bool FROM_VALS>
 static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, double* oval, int64_t* oidx,
                           hipStream_t st, Cand* ocand = nullptr) {
     const int64_t L = (int64_t)nl * q;
-    if (q <= kStreamMaxQ && (merge_reg_enabled() || ocand)) {
+    if (q <= kStreamMaxQ) {  // (the LDS-buffer merges below measured slower for q <= 64)
         hipLaunchKernelGGL((k_merge_reg<FROM_VALS>), dim3(segments), dim3(1024), 0, st, src, nl, q, oval, oidx,
                            ocand);
         return;

@@ -16,88 +16,43 @@ constexpr int small_ipt() { return Src::kC > 4 ? 2 : 4; }
 // reference's 4-member f64 committee, configs[0])
 template <class Src, int BS>
 constexpr int small_unr() { return (Src::kC > 4 || BS > 512) ? 2 : 4; }
-// the tiled A/B path is instantiated for the reference's committee shapes only
-// (vectorisable f32 / f64 rows of C = 4): 17 shapes x 3 block sizes of this
-// kernel doubled the library
-template <class Src>
-constexpr bool tiles_built() { return Src::kC == 4 && Src::kVec && Src::kDT != kBF16; }
 
-// Default: ONE block per problem (S = 1: the whole pool / user / mix selected
-// by one block, no hand-off).  Measured on MI355X (profiles/r03_small.json):
-// splitting a problem over S > 1 tiles with the arrival-ticket merge was
+// ONE block per problem (the whole pool / user / mix selected by one block,
+// no hand-off).  Measured on MI355X (profiles/r03_small.json): splitting a
+// problem over several blocks with an arrival-ticket merge of their lists was
 // slower at the reference's sizes -- the hand-off (write-through lists, one
-// agent-scope atomic, sc1 reads by the last tile) costs more than spreading
+// agent-scope atomic, sc1 reads by the last block) costs more than spreading
 // 1608 items over more CUs saves (C1 9.4 -> 11.1-13.0 us, C3 15.7 -> 19.0 us).
-// A/B knobs, items per tile (> 0 enables tiling): CE_AMD_TILE_POOL (one pool,
-// the hc table), CE_AMD_TILE_USER (batched users), CE_AMD_TILE_MIX (each mix
-// segment).
-static int64_t tile_target(const char* env) {
-    const char* e = getenv(env);
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (int64_t)v : 0;
-}
-static int64_t target_pool() {
-    static const int64_t v = tile_target("CE_AMD_TILE_POOL");
-    return v;
-}
-static int64_t target_user() {
-    static const int64_t v = tile_target("CE_AMD_TILE_USER");
-    return v;
-}
-static int64_t target_mix() {
-    static const int64_t v = tile_target("CE_AMD_TILE_MIX");
-    return v;
-}
-
-// tiles for `len` items at <= `target` per tile, within the merge's capacity
-static int tiles_for(int64_t len, int64_t target, int q, int smax) {
-    if (target <= 0) return 1;
-    int64_t s = cdiv(len < 1 ? 1 : len, target);
-    const int64_t cap = std::min<int64_t>(smax, kTileMergeCap / q);
-    if (s > cap) s = cap;
-    return (int)(s < 1 ? 1 : s);
-}
-
-template <class SrcA, class SrcB, int IPTA, int IPTB, int BS, int UNRA = small_unr<SrcA, BS>(), bool MERGE = true,
-          bool LONG = true>
+// LONG: a problem may exceed BS * IPT items (the per-wave streaming path is compiled in)
+template <class SrcA, class SrcB, int IPTA, int IPTB, int BS, int UNRA, bool LONG>
 static void launch_tiles(const SrcA& a, const SrcB& b, const TileArgs& ta, int problems, int q, double* oval,
                          int64_t* oidx, const uint32_t* excl, hipStream_t st) {
-    hipLaunchKernelGGL((k_select_tiles<SrcA, SrcB, IPTA, IPTB, UNRA, 1, BS, MERGE, LONG>),
-                       dim3((unsigned)(problems * (ta.SA + ta.SB))), dim3(BS), 0, st, a, b, ta, q, oval, oidx, excl);
+    hipLaunchKernelGGL((k_select_tiles<SrcA, SrcB, IPTA, IPTB, UNRA, 1, BS, LONG>), dim3((unsigned)problems), dim3(BS),
+                       0, st, a, b, ta, q, oval, oidx, excl);
 }
 
 bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval, int64_t* oidx, const uint32_t* excl,
                        WsLists w, hipStream_t st) {
+    (void)w;
     if (a.N < 1 || a.N > kSmallPoolItems) return false;
     bool launched = false;
     const int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
         constexpr int IPT = small_ipt<S>();
-        const int SA = tiles_for(a.N, target_pool(), q, 16);
-        const int64_t per = cdiv(a.N, SA);
-        const TileArgs ta{nullptr, a.N, 0, base_idx, SA, 0, w.c, w.ctr};
-        if (SA > 1) {
-            if constexpr (tiles_built<S>()) {
-                if (per > (int64_t)kTileBS * IPT) return;  // tiles would be long: not this path
-                launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, 1, q, oval, oidx, excl, st);
-            } else {
-                return;
-            }
-        } else if (per <= 512 * IPT) {  // one block; the pool fits it: no merge, no long path
+        const TileArgs ta{nullptr, a.N, 0, base_idx};
+        if (a.N <= 512 * IPT) {  // one block; the pool fits it: no long path
             if constexpr (S::kDT == kF64 && S::kC == 4) {
                 // one-member f64 tables (the hc select, amg_test.py:451-452): one load per
                 // item slot, not UNR copies of member 0 (measured 8.0 -> 7.3 us)
                 if (a.M == 1) {
-                    launch_tiles<S, S, IPT, 0, 512, 1, false, false>(src, src, ta, 1, q, oval, oidx, excl, st);
+                    launch_tiles<S, S, IPT, 0, 512, 1, false>(src, src, ta, 1, q, oval, oidx, excl, st);
                     launched = true;
                     return;
                 }
             }
-            launch_tiles<S, S, IPT, 0, 512, small_unr<S, 512>(), false, false>(src, src, ta, 1, q, oval, oidx, excl,
-                                                                                st);
-        } else if (per <= 1024 * IPT) {
-            launch_tiles<S, S, IPT, 0, 1024, small_unr<S, 1024>(), false, false>(src, src, ta, 1, q, oval, oidx, excl,
-                                                                                  st);
+            launch_tiles<S, S, IPT, 0, 512, small_unr<S, 512>(), false>(src, src, ta, 1, q, oval, oidx, excl, st);
+        } else if (a.N <= 1024 * IPT) {
+            launch_tiles<S, S, IPT, 0, 1024, small_unr<S, 1024>(), false>(src, src, ta, 1, q, oval, oidx, excl, st);
         } else {
             return;
         }
@@ -106,51 +61,30 @@ bool launch_small_pool(const CommArgs& a, int64_t base_idx, int q, double* oval,
     return rc == CE_OK && launched;
 }
 
-int small_users_tiles(int64_t total_items, int U, int q) {
-    if (U < 1) U = 1;
-    if (q < 1) q = 1;
-    return tiles_for(cdiv(total_items, U), target_user(), q, 16);
-}
-
 bool launch_small_users(const CommArgs& a, const int64_t* offsets, int U, int q, double* oval, int64_t* oidx,
-                        WsLists w, hipStream_t st) {
-    if (U < 1 || U > kWsCounters) return false;
-    const int SA = small_users_tiles(a.N, U, q);
+                        hipStream_t st) {
+    if (U < 1) return false;
     bool launched = false;
     const int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
         constexpr int IPT = small_ipt<S>();
-        // the average user must fit its tiles (a longer one streams inside its tile)
-        const int64_t per = cdiv(cdiv(a.N, U), SA);
-        const TileArgs ta{offsets, 0, 0, 0, SA, 0, w.c, w.ctr};
-        if (SA > 1) {
-            if constexpr (tiles_built<S>()) {
-                if (per > (int64_t)kTileBS * IPT) return;
-                launch_tiles<S, S, IPT, 0, kTileBS>(src, src, ta, U, q, oval, oidx, nullptr, st);
-            } else {
-                return;
-            }
-        } else {  // one 512-thread block per user: 2 per CU, all 500 users of configs[2] resident
-            if (per > (int64_t)512 * IPT) return;
-            launch_tiles<S, S, IPT, 0, 512, small_unr<S, 512>(), false, true>(src, src, ta, U, q, oval, oidx, nullptr,
-                                                                               st);
-        }
+        // one 512-thread block per user: 2 per CU, all 500 users of configs[2] resident;
+        // the average user must fit its block (a longer one streams inside it)
+        if (cdiv(a.N, U) > (int64_t)512 * IPT) return;
+        const TileArgs ta{offsets, 0, 0, 0};
+        launch_tiles<S, S, IPT, 0, 512, small_unr<S, 512>(), true>(src, src, ta, U, q, oval, oidx, nullptr, st);
         launched = true;
     });
     return rc == CE_OK && launched;
 }
 
 // mix: committee items (segment A) then the hc table rows (segment B, a
-// 1-member f64 committee), 2 items per thread per segment: one 1024-thread
-// block (S = 1, up to 2048 + 2048 rows) or 256-thread tiles
-bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, double* oval, int64_t* oidx, WsLists w,
-                      hipStream_t st) {
+// 1-member f64 committee), 2 items per thread per segment, in one 1024-thread
+// block (up to 2048 + 2048 rows)
+bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, double* oval, int64_t* oidx, hipStream_t st) {
     if (a.N < 1 || t.N < 1) return false;
-    const bool tiled = target_mix() > 0;
-    const int SA = tiles_for(a.N, target_mix(), q, 8), SB = tiles_for(t.N, target_mix(), q, 8);
-    const int BS = tiled ? kTileBS : 1024;
-    if (cdiv(a.N, SA) > 2 * BS || cdiv(t.N, SB) > 2 * BS || (SA + SB) * q > kTileMergeCap) return false;
-    const TileArgs ta{nullptr, a.N, t.N, 0, tiled ? SA : 1, tiled ? SB : 0, w.c, w.ctr};
+    if (a.N > 2 * 1024 || t.N > 2 * 1024) return false;
+    const TileArgs ta{nullptr, a.N, t.N, 0};
     bool launched = false;
     const int rc = with_committee(a, [&](auto src) {
         using S = decltype(src);
@@ -161,15 +95,8 @@ bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, double* oval,
             constexpr int UNRA = (S::kDT == kF64 || S::kC > 4) ? 2 : 4;
             auto go = [&](auto hsrc) {
                 using H = decltype(hsrc);
-                if (tiled) {
-                    if constexpr (tiles_built<S>())
-                        launch_tiles<S, H, 2, 2, kTileBS, UNRA>(src, hsrc, ta, 1, q, oval, oidx, nullptr, st);
-                } else {
-                    launch_tiles<S, H, 2, 2, 1024, UNRA, false, false>(
-                        src, hsrc, TileArgs{nullptr, a.N, t.N, 0, 1, 0, w.c, w.ctr}, 1, q, oval, oidx, nullptr, st);
-                }
+                launch_tiles<S, H, 2, 2, 1024, UNRA, false>(src, hsrc, ta, 1, q, oval, oidx, nullptr, st);
             };
-            if (tiled && !tiles_built<S>()) return;
             if (vec_ok(t, CC)) go(make_src<kF64, CC, true>(t));
             else go(make_src<kF64, CC, false>(t));
             launched = true;

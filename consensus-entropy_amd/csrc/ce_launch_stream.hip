@@ -18,24 +18,6 @@ static inline void with_batching(int M, F&& f) {
 }
 
 
-// A/B knob: CE_AMD_MNC_DMA=0 -> member-major pools on the direct-load kernel
-static bool mnc_dma_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_MNC_DMA");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// A/B knob: CE_AMD_FOLD=0 -> stage 2 as its own launch even where it can be folded
-static bool fold_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("CE_AMD_FOLD");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                               const uint32_t* excl, const FoldOut* fold);
 
@@ -46,12 +28,12 @@ bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w,
 
 int launch_stream_fold(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                        const uint32_t* excl, FoldOut out) {
-    return launch_stream_impl(a, G, q, base_idx, w, st, excl, fold_enabled() ? &out : nullptr);
+    return launch_stream_impl(a, G, q, base_idx, w, st, excl, &out);
 }
 
 static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                               const uint32_t* excl, const FoldOut* fold) {
-    if (!stream_enabled() || q > kStreamMaxQ || a.N == 0) return 0;
+    if (q > kStreamMaxQ || a.N == 0) return 0;
     StreamArgs sa = stream_args(a, G, base_idx);
     sa.excl = excl;
     if (fold) {  // kernels that fold read these; k_stream_wide (below) does not
@@ -68,7 +50,7 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     if (dense_nmc && (R == 256 || R == 512)) {
 #define CE_S(DT_, C_, S_)                                                                                   \
     if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
-        auto kern = dma_nt() ? k_stream_nmc<DT_, C_, S_, 2> : k_stream_nmc<DT_, C_, S_, 0>;              \
+        auto kern = k_stream_nmc<DT_, C_, S_, 2>;                                                         \
         const int grid = resident_grid(kern, 0, G);                                                       \
         stream_grid(sa, grid);                                                                            \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                               \
@@ -81,11 +63,11 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     // member-major stack (the reference's np.array(pred_prob) order) with
     // 16-B member rows: LDS-DMA tiles of one 1 KiB run per member
     const bool dense_mnc = a.sC == 1 && a.sN == a.C && a.C * eb == 16 && (a.sM * eb) % 16 == 0 &&
-                           (uintptr_t)a.p % 16 == 0 && a.M >= 4 && mnc_dma_enabled();
+                           (uintptr_t)a.p % 16 == 0 && a.M >= 4;
     if (dense_mnc) {
 #define CE_SM(DT_, C_, M_)                                                                              \
     if (a.dt == DT_ && a.C == C_ && a.M == M_) {                                                       \
-        auto kern = dma_nt() ? k_stream_nmc<DT_, C_, M_, 2, true> : k_stream_nmc<DT_, C_, M_, 0, true>; \
+        auto kern = k_stream_nmc<DT_, C_, M_, 2, true>;                                                \
         const int grid = resident_grid(kern, 0, G);                                                    \
         stream_grid(sa, grid);                                                                         \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                            \
@@ -113,47 +95,26 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
         constexpr int DT = decltype(dt)::value, NPL = decltype(npl)::value;
         if constexpr (decltype(vec)::value) {
-            // an item's member rows contiguous ([N, M, C], sM == C): LDS-DMA tiles
             constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
-            constexpr int TMAX = KCH >= 16 ? 1 : 16 / KCH;
-            const int R = a.C * eb;
-            if (wide_dma_enabled() && a.sM == a.C && R <= 16384) {
-                const int T = std::min(TMAX, 16384 / R);
-                const int tile = (T * R + 1023) / 1024 * 1024;
-                const int rowb = wide_lds_doubles(a.C) * 8;
-                const int bufb = (std::max(tile, rowb) + 15) / 16 * 16;
-                const size_t dl = (size_t)4 * bufb;
-                auto kern = dma_nt() ? k_stream_wide_dma<DT, KCH, 2> : k_stream_wide_dma<DT, KCH, 0>;
-                if (dl > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dl);
-                const int grid = resident_grid(kern, dl, G);
-                stream_grid(sa, grid);
-                sa.per_wave = cdiv(a.N, (int64_t)grid * 4);  // whole items
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), dl, st, wa, pl, sa, q, w.c, T, bufb);
+            // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
+            constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
+            // a 2-batch register ring (3 and 4 measured: 72.8 / 71.9 % vs 72.6 % at C5)
+            auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
+            const int grid = resident_grid(kern, lds, G);
+            stream_grid(sa, grid);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
+        } else {  // strided / unaligned rows: the unpipelined wave-per-item kernel
+            if (sa.excl) {  // k_stream_wide takes no bitmap
+                rc_excl = CE_EUNSUPPORTED;
                 return;
             }
-            if (wide2_enabled()) {
-                constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
-                // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
-                constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
-                // a 2-batch register ring (3 and 4 measured: 72.8 / 71.9 % vs 72.6 % at C5)
-                auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
-                const int grid = resident_grid(kern, lds, G);
-                stream_grid(sa, grid);
-                sa.per_wave = cdiv(a.N, (int64_t)grid * 4);  // whole items, not 64-item tiles
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
-                return;
-            }
+            sa.ctr = nullptr;  // ... and does not fold
+            wide_folded = false;
+            auto kern = k_stream_wide<DT, NPL, false>;
+            const int grid = resident_grid(kern, lds, G);
+            stream_grid(sa, grid);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
         }
-        if (sa.excl) {  // k_stream_wide takes no bitmap
-            rc_excl = CE_EUNSUPPORTED;
-            return;
-        }
-        sa.ctr = nullptr;  // ... and does not fold
-        wide_folded = false;
-        auto kern = k_stream_wide<DT, NPL, decltype(vec)::value>;
-        const int grid = resident_grid(kern, lds, G);
-        stream_grid(sa, grid);
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
     });
     if (rc != CE_OK || rc_excl != CE_OK) return 0;
     return wide_folded ? 2 : 1;

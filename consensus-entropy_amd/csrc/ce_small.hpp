@@ -1,37 +1,21 @@
 // ce_small.hpp -- pools of a few thousand items (BASELINE configs[0..2]: one
 // reference-sized pool, the hc table, the [mc; hc] mix, 500 users in one
-// launch) selected by TILES: a problem (the pool, a user, the mix) is cut into
-// S tiles, one block each, so a 1608-item pool is spread over several CUs
-// instead of one (round 2 ran each problem on one CU).  Every tile computes
-// its items' keys and its own exact top-q; the LAST tile of a problem to
-// finish (an arrival ticket in the workspace) merges the S sorted lists and
-// writes the problem's selection -- still ONE launch, no second kernel.
+// launch), each problem (the pool, a user, the mix) selected by ONE block:
 //
-// Per tile (amg_test.py:441-445 on the tile's items):
-//   1. the log table's loads are issued, then ALL member loads of the
-//      thread's IPT items (item lo + tid + BS*v: each wave's loads coalesced);
+// Per block (amg_test.py:441-445 on the problem's items):
+//   1. the log table's loads are issued, then the member loads of the
+//      thread's item slots (item lo + tid + BS*v: each wave's loads coalesced);
 //      each item's mean + entropy runs as soon as its own loads have landed;
 //   2. the best key of each group of BS/64 lanes (lane-exchange butterfly) ->
 //      64 group bests (distinct items) in LDS; every thread ranks one of them
 //      against a 1/W slice of the others; the group best of rank q-1 is an
 //      exact floor (q items are >= it);
 //   3. items >= the floor are appended to an LDS list (one atomic per wave);
-//      survivor t counts the survivors that beat it and writes itself to slot
-//      `rank` (< q) of the tile's sorted list (or of the final outputs when
-//      S = 1).
-// A tile longer than BS*IPT items (a long user of a ragged batch), or more
+//      survivor t counts the survivors that beat it and writes itself to
+//      output slot `rank` (< q).
+// A problem longer than BS*IPT items (a long user of a ragged batch), or more
 // than 64*W survivors (floods of exact ties at the floor), takes per-wave
 // register lists + a tree merge instead (block-uniform branches, same answer).
-//
-// Merge (S > 1): the tile lists are stored write-through and every tile
-// arrives on its problem's counter (arrive_last, ce_stream.hpp: no L2
-// write-back / invalidate); the last tile to arrive resets the counter for
-// the next call, loads the S*q candidates into LDS (sc1 loads), and ranks each candidate by
-// its slot in its own list + a binary search in each other list (all lists
-// are best-first; empty slots -- key 0, idx -1 -- sort after every real
-// candidate).  Counters live in the workspace header: zero before the first
-// call (the Python side allocates the workspace zero-filled; ce.h states the
-// contract) and zero again after every call.
 #pragma once
 #include "ce_stream.hpp"
 
@@ -51,21 +35,15 @@ __device__ uint64_t g_phase[8192][16];
 #define CE_WSTAMP(b)
 #endif
 
-// Geometry of a tiled launch: block b is tile t = b % S of problem p = b / S,
-// S = SA + SB.  Tiles [0, SA) split segment A (committee items: one pool
-// [0, n) or user p's [offsets[p], offsets[p+1])), tiles [SA, S) split segment
-// B (the mix's hc rows [0, nB)).
+// Geometry: block p selects problem p -- segment A (committee items: one
+// pool [0, n) or user p's [offsets[p], offsets[p+1])) and, for the mix,
+// segment B (the hc rows [0, nB), positions n + row).
 struct TileArgs {
     const int64_t* offsets;  // [P+1] problem offsets (batched users), or nullptr: one problem
     int64_t n;               // segment-A items (offsets == nullptr)
     int64_t nB;              // segment-B rows (mix), 0 otherwise
     int64_t base_idx;        // position of item 0 (offsets == nullptr)
-    int SA, SB;              // tiles per problem over segment A / B
-    Cand* lists;             // [P*S][q] tile lists (S > 1)
-    uint32_t* ctr;           // [P] arrival counters (S > 1): 0 at rest
 };
-
-constexpr int kTileMergeCap = 1024;  // S * q candidates a merge holds (host: S <= kTileMergeCap / q)
 
 template <int WAVES>
 struct TileSmem {
@@ -74,17 +52,9 @@ struct TileSmem {
     int64_t gi[64];
     int part[WAVES][64];                    // partial ranks of the group bests
     int cnt;                                // survivors appended
-    int ticket;                             // arrival ticket of this tile (S > 1)
-    int nvalid;                             // merge: real candidates over all lists
     uint64_t ck[CAP];
     int64_t ci[CAP];
-    union {
-        WaveListsT<WAVES> lists;            // fallback tree merge
-        struct {
-            uint64_t k[kTileMergeCap];
-            int64_t i[kTileMergeCap];
-        } m;                                // the S lists of a problem (merge)
-    };
+    WaveListsT<WAVES> lists;                // fallback tree merge
 };
 
 // Keys of this thread's IPT items lo + tid + BS*v of [lo, hi) into slots
@@ -123,11 +93,10 @@ __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi
     }
 }
 
-// MERGE: launched with S > 1 tiles per problem (the ticketed merge is compiled
-// in); LONG: a tile may exceed BS * IPT items (the per-wave streaming path is
-// compiled in).  Single-block launches whose host checks bound the problem
-// (one pool, the mix) drop both -- half the code of the kernel.
-template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS, bool MERGE = true, bool LONG = true>
+// LONG: a problem may exceed BS * IPT items (the per-wave streaming path is
+// compiled in).  Launches whose host checks bound the problem (one pool, the
+// mix) drop it -- half the code of the kernel.
+template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS, bool LONG = true>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_select_tiles(
     SrcA srcA, SrcB srcB, TileArgs ta, int q, double* __restrict__ oval, int64_t* __restrict__ oidx,
     const uint32_t* __restrict__ excl) {
@@ -140,36 +109,19 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     LogTablePrefetch tab;
     tab.fetch();
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int S = ta.SA + ta.SB;
-    const int p = blockIdx.x / S, t = blockIdx.x - p * S;
-    const int64_t s0 = ta.offsets ? ta.offsets[p] : 0, s1 = ta.offsets ? ta.offsets[p + 1] : ta.n;
-    const int64_t lenA = s1 > s0 ? s1 - s0 : 0;
-    const int64_t rel = (ta.offsets ? 0 : ta.base_idx) - s0;  // A: position = item + rel
+    const int p = blockIdx.x;
+    const int64_t lo = ta.offsets ? ta.offsets[p] : 0, hi0 = ta.offsets ? ta.offsets[p + 1] : ta.n;
+    const int64_t hi = hi0 > lo ? hi0 : lo;
+    const int64_t rel = (ta.offsets ? 0 : ta.base_idx) - lo;  // A: position = item + rel
     const int64_t relB = ta.n + ta.base_idx;                  // B: position = row + relB
-    const bool segB = IPTB > 0 && t >= ta.SA;                 // block-uniform
-    // the mix in ONE block (SB == 0 with a segment B): the block takes every
-    // committee item AND every hc row (slots [0, IPTA) and [IPTA, K))
-    const bool both = IPTB > 0 && ta.SB == 0 && ta.nB > 0;
-    int64_t lo, hi;
-    if (!segB) {
-        const int64_t per = (lenA + ta.SA - 1) / ta.SA;
-        lo = s0 + (int64_t)t * per;
-        hi = lo + per < s1 ? lo + per : s1;
-    } else {
-        const int64_t per = (ta.nB + ta.SB - 1) / ta.SB;
-        lo = (int64_t)(t - ta.SA) * per;
-        hi = lo + per < ta.nB ? lo + per : ta.nB;
-    }
-    if (lo > hi) lo = hi;
-    const bool direct = !MERGE || S == 1;  // the tile is the whole problem: final outputs, no merge
+    // the mix: the block takes every committee item AND every hc row (slots [0, IPTA) and [IPTA, K))
+    const bool both = IPTB > 0 && ta.nB > 0;
     double* ov = oval + (int64_t)p * q;
     int64_t* oi = oidx + (int64_t)p * q;
-    Cand* lst = ta.lists + (int64_t)blockIdx.x * q;
     CE_DASSERT(q >= 1 && q <= 64);
-    CE_DASSERT(direct || (int64_t)S * q <= kTileMergeCap);
 
     const bool long_tile = both ? (hi - lo > (int64_t)BS * IPTA || ta.nB > (int64_t)BS * IPTB)
-                                : hi - lo > (int64_t)BS * (segB ? IPTB : IPTA);
+                                : hi - lo > (int64_t)BS * IPTA;
     CE_DASSERT(LONG || !long_tile);
     if (LONG && long_tile) {  // block-uniform: per-wave streams + tree merge
         tab.commit();
@@ -184,20 +136,13 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         };
         int64_t wlo, whi;
         wave_part(lo, hi, wlo, whi);
-        if (!segB) {
-            stream_direct_range<SrcA, 2, UNRA>(srcA, wlo, whi, rel, q, tq, excl);
-        } else {
-            if constexpr (IPTB > 0) stream_direct_range<SrcB, 2, UNRB>(srcB, wlo, whi, relB, q, tq, nullptr);
-        }
+        stream_direct_range<SrcA, 2, UNRA>(srcA, wlo, whi, rel, q, tq, excl);
         if (both) {
             wave_part(0, ta.nB, wlo, whi);
             if constexpr (IPTB > 0) stream_direct_range<SrcB, 2, UNRB>(srcB, wlo, whi, relB, q, tq, nullptr);
         }
-        if (direct) {
-            block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
-            return;
-        }
-        block_merge_write<W>(tq, sm.lists, q, lst, 0, nullptr, nullptr, W, true);
+        block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
+        return;
     } else {
         // 1. keys of this thread's items
         uint64_t k[K];
@@ -209,14 +154,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
             pos[v] = INT64_MAX;
             ok[v] = false;
         }
-        if (!segB) {
-            tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, rel, excl, tab, k, pos, ok);
-            if constexpr (IPTB > 0)
-                if (both) tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, false>(srcB, 0, ta.nB, relB, nullptr, tab, k, pos, ok);
-        } else {
-            if constexpr (IPTB > 0)
-                tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, true>(srcB, lo, hi, relB, nullptr, tab, k, pos, ok);
-        }
+        tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, rel, excl, tab, k, pos, ok);
+        if constexpr (IPTB > 0)
+            if (both) tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, false>(srcB, 0, ta.nB, relB, nullptr, tab, k, pos, ok);
         CE_STAMP(blockIdx.x, 1)
         CE_WSTAMP(blockIdx.x)
         uint64_t bk = 0;
@@ -301,82 +241,23 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 // (batching 8 LDS reads per step measured slower: rank 0.64 -> 0.80 us)
                 for (int j = 0; j < nc; ++j) r += better(sm.ck[j], sm.ci[j], mk, mi);
                 if (r < q) {
-                    if (direct) {
-                        ov[r] = key_to_val(mk);
-                        oi[r] = mi;
-                    } else {
-                        store_cand_wt(lst + r, mk, mi);
-                    }
+                    ov[r] = key_to_val(mk);
+                    oi[r] = mi;
                 }
             } else if (tid < q) {  // fewer survivors than q: padding
-                if (direct) {
-                    ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
-                    oi[tid] = -1;
-                } else {
-                    store_cand_wt(lst + tid, 0ull, -1);
-                }
+                ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
+                oi[tid] = -1;
             }
             CE_STAMP(blockIdx.x, 4)
-            if (direct) return;
         } else {
             // overflow (> CAP items tie at or above the floor): per-wave lists + tree merge
             RegTopQ tq;
             tq.init(q, fk, fi == INT64_MAX ? fi : fi + 1);  // admit candidates >= the floor
 #pragma unroll
             for (int v = 0; v < K; ++v) tq.offer(k[v], pos[v], ok[v]);
-            if (direct) {
-                block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
-                return;
-            }
-            block_merge_write<W>(tq, sm.lists, q, lst, 0, nullptr, nullptr, W, true);
+            block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
         }
     }
-
-    // ---- arrival ticket: the last tile of problem p merges the S lists ----
-    if constexpr (!MERGE) return;
-    if (!arrive_last(ta.ctr + p, (uint32_t)S, &sm.ticket)) return;  // block-uniform
-    if (tid == 0) sm.nvalid = 0;
-    const Cand* L = ta.lists + (int64_t)p * S * q;
-    const int nL = S * q;
-    for (int j = tid; j < nL; j += BS) {  // handed off in this launch: sc1 loads only
-        const Cand c = load_cand_wt(L + j);
-        sm.m.k[j] = c.key;
-        sm.m.i[j] = c.idx;
-    }
-    __syncthreads();
-    for (int j0 = 0; j0 < nL; j0 += BS) {  // block-uniform bound
-        const int j = j0 + tid;
-        const bool valid = j < nL && sm.m.i[j] >= 0;
-        const uint64_t vm = __ballot(valid);
-        if (lane == 0 && vm) atomicAdd(&sm.nvalid, __popcll(vm));
-        if (valid) {
-            const uint64_t ck = sm.m.k[j];
-            const int64_t cidx = sm.m.i[j];
-            const int a = j / q;
-            int rank = j - a * q;  // its slot in its own list
-            for (int b = 0; b < S; ++b) {
-                if (b == a) continue;
-                // entries of list b better than (ck, cidx): a prefix of the list
-                int l = 0, h = q;
-                while (l < h) {
-                    const int mid = (l + h) >> 1;
-                    if (better(sm.m.k[b * q + mid], sm.m.i[b * q + mid], ck, cidx)) l = mid + 1;
-                    else h = mid;
-                }
-                rank += l;
-            }
-            if (rank < q) {
-                ov[rank] = key_to_val(ck);
-                oi[rank] = cidx;
-            }
-        }
-    }
-    __syncthreads();
-    for (int r = sm.nvalid + tid; r < q; r += BS) {  // fewer real candidates than q: padding
-        ov[r] = __longlong_as_double(0x7ff8000000000000ll);
-        oi[r] = -1;
-    }
-    CE_STAMP(blockIdx.x, 5)
 }
 
 }  // namespace ce

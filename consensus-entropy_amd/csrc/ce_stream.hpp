@@ -366,7 +366,6 @@ struct StreamArgs {
     int64_t per_wave;  // items per wave (multiple of 64)
     const uint32_t* excl;  // exclusion bitmap over items 0..N-1 (1 = out of the pool), or nullptr
     int nlists;        // workspace lists (>= gridDim.x); lists past the grid are written empty
-    int ileave;        // k_stream_nmc tile order: -1 the layout's default, 0 runs, 1 block-interleaved, 2 grid-cyclic
     // stage 2 folded in (ctr != nullptr): the last block merges the grid's
     // lists into (oval, oidx), or into q records at ocand
     uint32_t* ctr;
@@ -401,19 +400,19 @@ __device__ __forceinline__ Cand load_cand_wt(const Cand* p) {
     return c;
 }
 // Every thread of the block calls it after its write-through stores; true in
-// every thread of the block whose arrival is the n-th (that block resets the
-// counter to 0 for the next call: all n arrivals have happened).
+// every thread of the block whose arrival is the n-th.  The counter wraps
+// itself: global_atomic_inc with limit n - 1 returns 0..n-1 and stores 0 after
+// the n-th arrival, so the counter is zero again once every block has arrived
+// (and stays in [0, n) even when a misuse -- two launches sharing one
+// workspace -- interleaves their arrivals: it does not stay broken).
 __device__ __forceinline__ bool arrive_last(uint32_t* ctr, uint32_t n, int* lds_ticket) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
-        *lds_ticket = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) *lds_ticket = (int)__builtin_amdgcn_atomic_inc32(ctr, n - 1, __ATOMIC_RELAXED, "agent");
     __syncthreads();
     const int t = *lds_ticket;
     CE_DASSERT(t >= 0 && t < (int)n);
-    const bool last = t == (int)n - 1;
-    if (last && threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return last;
+    return t == (int)n - 1;
 }
 
 // wt: the list at wc is read inside this launch (a fold / tile merge): store
@@ -740,25 +739,20 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     int64_t lo, hi, step;
     // tile distribution (measured on two boxes, alternating runs,
     // profiles/r03_tile_order.json): item-major -- grid-cyclic, equal on a box
-    // where contiguous runs reach 0.871 and +2.5 % (0.836 -> 0.859) on one where
-    // they reach only 0.836; member-major -- block-interleaved (+0.3-0.5 %),
-    // grid-cyclic 4 % slower there
-    const int mode = a.ileave >= 0 ? a.ileave : (MNC ? 1 : 2);
-    if (mode == 2) {  // grid-cyclic: wave g takes tiles g, g + W, g + 2W, ... (W = the grid's waves), so
+    // where a contiguous run per wave reaches 0.871 and +2.5 % (0.836 -> 0.859)
+    // on one where it reaches only 0.836; member-major -- block-interleaved
+    // (+0.3-0.5 % over runs), grid-cyclic 4 % slower there
+    if constexpr (!MNC) {  // grid-cyclic: wave g takes tiles g, g + W, g + 2W, ... (W = the grid's waves), so
         // the tiles in flight at any moment form one contiguous sweep of the pool
         const int64_t W = (int64_t)gridDim.x * 4;
         lo = ((int64_t)blockIdx.x * 4 + w) * 64;
         hi = a.N;
         step = W * 64;
-    } else if (mode == 1) {  // the block's 4 waves take alternate tiles of the block's run (adjacent bursts per member row)
+    } else {  // the block's 4 waves take alternate tiles of the block's run (adjacent bursts per member row)
         const int64_t blo = (int64_t)blockIdx.x * 4 * a.per_wave;
         hi = blo + 4 * a.per_wave < a.N ? blo + 4 * a.per_wave : a.N;
         lo = blo + 64 * w;
         step = 256;
-    } else {  // each wave a contiguous run
-        lo = ((int64_t)blockIdx.x * 4 + w) * a.per_wave;
-        hi = lo + a.per_wave < a.N ? lo + a.per_wave : a.N;
-        step = 64;
     }
     if (lo > hi) lo = hi;
     RegTopQ tq;

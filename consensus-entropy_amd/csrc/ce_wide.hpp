@@ -169,11 +169,10 @@ __device__ inline double wave_item_entropy(const void* p, int64_t off, int M, in
     __builtin_amdgcn_wave_barrier();
     const double s = wave_row_sum(row, pl, scratch);
     __builtin_amdgcn_wave_barrier();
-    const RowDivisor d(s);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int c = lane + 64 * k;
-        if (c < C) row[rp(c)] = entr(d.div(1.0 * acc[k]));
+        if (c < C) row[rp(c)] = entr(1.0 * acc[k] / s);
     }
     __builtin_amdgcn_wave_barrier();
     const double h = wave_row_sum(row, pl, scratch);
@@ -235,51 +234,12 @@ __device__ __forceinline__ double wave_entropy_from_sums(double* acc, int K, dou
     __builtin_amdgcn_wave_barrier();
     const double s = wave_row_sum(row, pl, scratch);
     __builtin_amdgcn_wave_barrier();
-    const RowDivisor d(s);  // the row's quotients share the divisor's reciprocal (ce_device.hpp)
 #pragma unroll
     for (int kk = 0; kk < KCH; ++kk) {
         const int ch = lane + 64 * kk;
 #pragma unroll
         for (int e = 0; e < CPC; ++e)
-            if (ch < K) row[rp(ch * CPC + e)] = entr(d.div(1.0 * acc[kk * CPC + e]));
-    }
-    __builtin_amdgcn_wave_barrier();
-    const double h = wave_row_sum(row, pl, scratch);
-    __builtin_amdgcn_wave_barrier();
-    return h;
-}
-
-// The same, with the entr pass fed from the LDS row instead of the
-// accumulator registers: the sums die once the mean row is written, and the
-// 16 entr of a lane run two at a time -- the entropy phase's register peak
-// drops below the streaming phase's (acc + the load ring), so the streaming
-// kernel keeps more waves per SIMD and more bytes in flight.
-template <int DT, int KCH>
-__device__ __forceinline__ double wave_entropy_from_sums_lds(double* acc, int K, double dM, double invM, bool pow2,
-                                                            const PwPlan& pl, double* row, double* scratch) {
-    constexpr int CPC = ChunkT<DT>::CPC;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int kk = 0; kk < KCH; ++kk) {
-        const int ch = lane + 64 * kk;
-#pragma unroll
-        for (int e = 0; e < CPC; ++e)
-            if (ch < K) row[rp(ch * CPC + e)] = div_members(acc[kk * CPC + e], dM, invM, pow2);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const double s = wave_row_sum(row, pl, scratch);
-    __builtin_amdgcn_wave_barrier();
-    const RowDivisor d(s);
-#pragma unroll 1
-    for (int kk = 0; kk < KCH; ++kk) {
-        const int ch = lane + 64 * kk;
-        if (ch < K) {
-#pragma unroll 2
-            for (int e = 0; e < CPC; ++e) {
-                double* x = row + rp(ch * CPC + e);
-                *x = entr(d.div(1.0 * *x));
-            }
-        }
+            if (ch < K) row[rp(ch * CPC + e)] = entr(1.0 * acc[kk * CPC + e] / s);
     }
     __builtin_amdgcn_wave_barrier();
     const double h = wave_row_sum(row, pl, scratch);

@@ -334,21 +334,6 @@ def test_wide_stream_vs_oracle(ce, N, M, C, dt):
     assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
 
 
-def test_wide_dma_stream_vs_oracle():
-    """The LDS-DMA wide stream (k_stream_wide_dma, an A/B build-time-free knob:
-    CE_AMD_WIDE_DMA=1, read once per process) through the same oracle tests as
-    the default register-ring stream, in a child process with the knob set."""
-    import subprocess
-    import sys
-
-    env = dict(os.environ, CE_AMD_WIDE_DMA="1")
-    r = subprocess.run([sys.executable, "-m", "pytest", os.path.abspath(__file__), "-q", "-x", "-m", "gpu",
-                        "-k", "wide_stream_vs_oracle or chunked_pool_vs_oracle", "-p", "no:cacheprovider"],
-                       env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout
-
-
 def test_frames_dma_tiles_vs_oracle():
     """ce_select_frames with the grouped members staged by LDS-DMA tiles
     (k_frames_lanes<C, true>; by default only pools with >= 4 steps per wave

@@ -64,3 +64,67 @@ def test_dynamo_traces_one_node(tops):
     compiled = torch.compile(step, backend="eager", fullgraph=True)
     assert torch.equal(compiled(P, hc), step(P, hc))
     assert np.all(step(P, hc).cpu().numpy() >= 0)
+
+
+def _oracle_idx(P, q):
+    from oracle import ce_oracle as O
+
+    return O.oracle_topq(O.oracle_committee_entropy(P.cpu().numpy(), "NMC"), q)[1]
+
+
+def _idx(t):
+    i = t.cpu().numpy()
+    return i[i >= 0]
+
+
+def test_two_streams_concurrently(tops):
+    """ops.select_mc / select_batched issued back to back on two streams over
+    different pools (the folded selection's arrival counters live in the
+    workspace: one workspace per (device, stream), include/ce.h): every call on
+    either stream equals the oracle."""
+    import ce_amd.ops as ops
+
+    Pa, Pb = pool(11, (1_000_000, 16, 4)), pool(12, (900_000, 16, 4))
+    exp_a, exp_b = _oracle_idx(Pa, 10), _oracle_idx(Pb, 10)
+    Ua = pool(13, (4, 500 * 1608, 4))
+    offs = torch.arange(0, 500 * 1608 + 1, 1608, device="cuda", dtype=torch.int64)
+    _, ub_ref = ops.select_batched(Ua, offs, 10, "MNC")
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs_a, outs_b, outs_u = [], [], []
+    for _ in range(12):
+        with torch.cuda.stream(sa):
+            outs_a.append(ops.select_mc(Pa, 10, "NMC")[1])
+            outs_u.append(ops.select_batched(Ua, offs, 10, "MNC")[1])
+        with torch.cuda.stream(sb):
+            outs_b.append(ops.select_mc(Pb, 10, "NMC")[1])
+    torch.cuda.synchronize()
+    for i in outs_a:
+        assert np.array_equal(_idx(i), exp_a)
+    for i in outs_b:
+        assert np.array_equal(_idx(i), exp_b)
+    for i in outs_u:
+        assert torch.equal(i, ub_ref)
+
+
+def test_graph_replay_after_cache_growth(tops):
+    """A captured selection keeps its own workspace: an eager call that grows
+    the (device, stream) workspace cache after the capture does not free
+    memory the graph uses, and the replay still equals the oracle."""
+    import ce_amd.ops as ops
+
+    P = pool(21, (200_000, 16, 4))
+    ops.select_mc(P, 10, "NMC")  # an eager call first: the cache holds a small buffer
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        v, i = torch.ops.ce_amd.select_mc(P, 10, "NMC", 0)
+    big = pool(22, (3_000_000, 16, 4))
+    _, ib = ops.select_mc(big, 64, "NMC")  # grows the eager workspace (64-slot block lists)
+    torch.cuda.synchronize()
+    assert np.array_equal(_idx(ib), _oracle_idx(big, 64))
+    P.copy_(pool(23, P.shape))
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(_idx(i), _oracle_idx(P, 10))

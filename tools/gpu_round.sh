@@ -1,12 +1,17 @@
 #!/bin/bash
 # One GPU visit, in phases (each GPU step has its own limit; a fault, abort or
 # time-out ends the script -- nothing more runs on the GPU in that call).
-#   PHASE=check    pytest -m gpu, smoke(), bench.py (default line + A/B lines)
-#   PHASE=profile  rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
-#   PHASE=xgb      the same for the XGB member (tools/bench_configs.py --only 7)
-#   PHASE=small    kernel traces of the small-pool configs + PMC passes of one (tools/small_probe.py)
+#   PHASE=check      pytest -m gpu, smoke(), bench.py (default line + A/B lines)
+#   PHASE=ab         bench.py A/B lines only (AB="name:ENV=v:--arg%value ...")
+#   PHASE=profile    rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes of bench.py (LAYOUT=NMC|MNC)
+#   PHASE=benchprof  rocprofv3 of EXACTLY the driver's bench command + FETCH / WRITE passes
+#   PHASE=configs    kernel traces of tools/bench_configs.py + FETCH / WRITE of the wide config
+#   PHASE=xgb        the same for the XGB member (tools/bench_configs.py --only 7)
+#   PHASE=mpmc       PMC passes over the member kernels (tools/members_pmc.py)
+#   PHASE=small      kernel traces of the small-pool configs + PMC passes of one (tools/small_probe.py)
+#   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
+#   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
-#   PHASE=debug    pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 # Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -108,10 +113,14 @@ debug)  # the whole GPU suite once on the debug build (device bounds checks: mak
   CE_AMD_LIB=$ROOT/tools/_diag/libce_amd_debug.so timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest_gpu_debug.log" 2>&1
   step $? "pytest debug build"
   ;;
+phase)  # per-block phase stamps of the C3 selection (tools/phase_probe.py) on the diagnostic build (make phase)
+  CE_AMD_LIB=$ROOT/tools/_diag/ce_amd_phase.so timeout -k 10 120 python3 tools/phase_probe.py > "$OUT/phase.json" 2> "$OUT/phase.err"
+  step $? "phase probe"
+  ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb or mpmc" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, debug, phase or firstcall" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
