@@ -22,8 +22,7 @@ LIB_PATH = os.environ.get("CE_AMD_LIB") or os.path.join(_HERE, "libce_amd.so")
 
 CE_OK, CE_EINVAL, CE_EWORKSPACE, CE_ELAUNCH, CE_EUNSUPPORTED = 0, -1, -2, -3, -4
 CE_F32, CE_F64, CE_BF16 = 0, 1, 2
-CE_MAX_Q = 2048
-CE_CAND_MAX_Q = 64  # ce_select_finish_cands / ce_merge_cands
+CE_MAX_Q = 2048  # the list kernels' q; any larger q runs on the sort path (include/ce.h)
 
 # name -> (restype, argtypes); the exact export list of include/ce.h
 _vp, _i64, _i32, _sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t

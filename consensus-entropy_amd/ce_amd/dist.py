@@ -9,7 +9,7 @@ subset of the union of the local top-qs, and the merge uses the same total
 order (NaN first, entropy descending, lowest position).
 
 Two exchange formats: (f64 entropy, i64 position) pairs packed into one i64
-tensor (any q), or -- for q <= 64, what bench.py uses -- the engine's 16-byte
+tensor, or -- what bench.py uses -- the engine's 16-byte
 candidate records (ce_cand), written by stage 2 straight into the all-gather
 send buffer and merged from the receive buffer as is (no pack/unpack kernels).
 The local-select and merge steps are injectable so the collective logic can be
@@ -100,7 +100,7 @@ def allgather_cands(cands, group=None, out=None):
 
 def sharded_select_mc_records(P_local, q, *, global_offset, layout="NMC", group=None, local_records=None,
                               merge_records=None):
-    """sharded_select_mc over the record exchange (q <= 64): stage 1 + stage 2
+    """sharded_select_mc over the record exchange (any q): stage 1 + stage 2
     write this rank's q records straight into the all-gather send buffer, and
     the merge reads the receive buffer.
 
@@ -214,7 +214,7 @@ def sharded_select_mc_chunks(chunks, q, *, layout="NMC", group=None, job=None, m
     """A pool larger than HBM (BASELINE configs[4]) over several GPUs: this
     rank streams ITS chunks -- ``chunks`` yields (device tensor, global
     base_idx) pairs, e.g. chunk c on rank c % world -- into a running top-q
-    (ops.MCChunkJob, q <= 64), then ONE all-gather of every rank's q running
+    (ops.MCChunkJob, any q), then ONE all-gather of every rank's q running
     records and the same merge on every rank.  A rank with no chunk contributes
     an empty list.  ``job``/``merge_records`` are injectable for CPU tests."""
     if job is None:

@@ -198,7 +198,8 @@ def select_frames(members, offsets, q, perm=None, base_idx=0, song_level=None):
     top-q over songs -- the [M, N, C] stack is never written.  ``members``:
     device tensors [F, C] (frame rows, song n = rows perm[offsets[n]:
     offsets[n+1]] or offsets[n]:offsets[n+1]) or [N, C] (song-level, e.g. the
-    CNN member); ``song_level`` overrides the shape rule per member.  q <= 64.
+    CNN member); ``song_level`` overrides the shape rule per member.  Any q:
+    q <= 64 in one pass; larger q through the per-song entropies.
     Returns (vals [q], idx [q]) over the N sorted songs."""
     members = list(members)
     if not members:
@@ -336,9 +337,12 @@ def xgb_predict_proba(X, forest, out=None, out_dtype=torch.float32):
 
 
 def _check_q(q):
+    """Any q >= 0, as the reference's -q (amg_test.py:547-553).  Outputs hold q
+    slots (padding -- val NaN, idx -1 -- past the pool); q <= CE_MAX_Q runs on
+    the list kernels, larger q on the sort path (workspace grows with N)."""
     q = int(q)
-    if q < 1 or q > _lib.CE_MAX_Q:
-        raise ValueError(f"q={q} outside [1, {_lib.CE_MAX_Q}]")
+    if q < 0:
+        raise ValueError(f"q={q} is negative")
     return q
 
 
@@ -368,7 +372,9 @@ def topq_merge(vals, idx, q):
     q = _check_q(q)
     vals = vals.contiguous().view(-1)
     idx = idx.contiguous().view(-1)
-    if vals.numel() != idx.numel() or vals.numel() % q:
+    if q == 0:
+        return _outs(0, vals.device)
+    if vals.numel() != idx.numel() or vals.numel() == 0 or vals.numel() % q:
         raise ValueError("vals/idx must hold nlists * q entries")
     ov, oi = _outs(q, vals.device)
     call("ce_topq_merge", _p(vals), _p(idx), vals.numel() // q, q, _p(ov), _p(oi), _stream(vals.device))
@@ -378,7 +384,7 @@ def topq_merge(vals, idx, q):
 def select_mc(P, q, layout="MNC", base_idx=0, excl=None):
     """Fused amg_test.py:441-445: (vals [q], idx [q]) best-first.  excl: an
     optional exclusion bitmap (int32 [ceil(N/32)], bit i set = item i is out
-    of the pool; q <= 64), see excl_bitmap / mark_selected."""
+    of the pool), see excl_bitmap / mark_selected."""
     N, M, C, sN, sM, sC, dt = committee_view(P, layout)
     q = _check_q(q)
     lib = _lib.load()
@@ -443,22 +449,22 @@ class MCPlan:
     def finish_cands(self, out=None):
         """Stage 2 writing this pool's q candidate records (ce_cand: order key,
         position; as an int64 [q, 2] tensor) -- the all-gather send buffer of
-        the multi-GPU merge.  q <= 64."""
+        the multi-GPU merge.  partial() / finish*() need q <= CE_MAX_Q."""
         if out is None:
             out = torch.empty((self.q, 2), dtype=torch.int64, device=self.P.device)
         call("ce_select_finish_cands", self.N, self.q, _p(self.ws), self.ws_bytes, _p(out), _stream(self.P.device))
         return out
 
     def step(self):
-        """The whole selection in ONE launch (ce_select_mc: stage 2 folded into
-        stage 1's last block for q <= 64): (vals [q], idx [q])."""
+        """The whole selection (ce_select_mc; ONE launch for q <= 64: stage 2
+        folded into stage 1's last block): (vals [q], idx [q])."""
         call("ce_select_mc", _p(self.P), self.dt, self.N, self.M, self.C, self.sN, self.sM, self.sC, self.q,
              self.base_idx, _p(self.ws), self.ws_bytes, _p(self.vals), _p(self.idx), _stream(self.P.device))
         return self.vals, self.idx
 
     def step_cands(self, out=None):
         """This pool's q candidate records (int64 [q, 2], the multi-GPU send
-        buffer) in ONE launch (ce_select_mc_cands).  q <= 64."""
+        buffer; ce_select_mc_cands, ONE launch for q <= 64)."""
         if out is None:
             out = torch.empty((self.q, 2), dtype=torch.int64, device=self.P.device)
         call("ce_select_mc_cands", _p(self.P), self.dt, self.N, self.M, self.C, self.sN, self.sM, self.sC, self.q,
@@ -475,12 +481,12 @@ def merge_cands(cands, q):
     into the final (vals [q], idx [q])."""
     _on_gpu(cands, "cands")
     q = _check_q(q)
-    if q > _lib.CE_CAND_MAX_Q:
-        raise ValueError(f"candidate records need q <= {_lib.CE_CAND_MAX_Q}")
     if cands.dtype != torch.int64 or cands.shape[-1] != 2 or not cands.is_contiguous():
         raise ValueError("cands must be a contiguous int64 [..., 2] tensor of records")
     n = cands.numel() // 2
-    if n % q:
+    if q == 0 or n == 0 or n % q:
+        if q == 0:
+            return _outs(0, cands.device)
         raise ValueError("cands must hold nlists * q records")
     ov, oi = _outs(q, cands.device)
     call("ce_merge_cands", _p(cands), n // q, q, _p(ov), _p(oi), _stream(cands.device))
@@ -493,12 +499,10 @@ class MCChunkJob:
     (pool positions continue from the previous chunk) and folds its top-q into
     a running list of q candidate records on the device; ``result()`` is the
     selection over everything added -- identical to select_mc on the whole
-    pool, ties included (q <= 64)."""
+    pool, ties included (any q)."""
 
     def __init__(self, q, layout="NMC", device=None):
         self.q = _check_q(q)
-        if self.q > _lib.CE_CAND_MAX_Q:
-            raise ValueError(f"chunked selection needs q <= {_lib.CE_CAND_MAX_Q}")
         self.layout = layout
         self.device = torch.device(device) if device is not None else None
         self.running = None

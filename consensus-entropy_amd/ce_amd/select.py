@@ -185,10 +185,8 @@ def select_queries(mode, q, *, committee=None, hc=None, votes=None, pool=None, r
     if mode not in MODES:
         raise ValueError(f"mode must be one of {MODES}, got {mode!r}")
     q = int(q)
-    if q < 1:
-        raise ValueError("q must be >= 1")
-    if q > ops._lib.CE_MAX_Q and mode != "rand":
-        raise ValueError(f"q = {q} exceeds the engine's CE_MAX_Q = {ops._lib.CE_MAX_Q} queries per call")
+    if q < 0:  # any other q is the reference's -q (amg_test.py:547-553): argsort[::-1][:q] keeps min(q, N)
+        raise ValueError(f"q = {q} is negative")
     if mode == "rand":
         if pool is None:
             raise ValueError("rand mode needs `pool`")
@@ -200,20 +198,26 @@ def select_queries(mode, q, *, committee=None, hc=None, votes=None, pool=None, r
         if committee is None:
             raise ValueError("mc mode needs `committee`")
         P, lay = stack_committee(committee, dev, layout)
-        _, idx = ops.select_mc(P, q, lay)
+        _, idx = ops.select_mc(P, min(q, _items(P, lay)), lay)
         return _positions(idx)
     if mode == "hc":
         H = _hc_tensor(hc, votes, n_classes, dev)
         P = H.unsqueeze(1)  # [N_h, M=1, C]: mean over one member is the row itself
-        _, idx = ops.select_mc(P, q, "NMC")
+        _, idx = ops.select_mc(P, min(q, H.shape[0]), "NMC")
         return _positions(idx)
     # mix
     if committee is None:
         raise ValueError("mix mode needs `committee`")
     P, lay = stack_committee(committee, dev, layout)
     H = _hc_tensor(hc, votes, n_classes, dev)
-    _, idx = ops.select_mix(P, H, q, lay)
+    _, idx = ops.select_mix(P, H, min(q, _items(P, lay) + H.shape[0]), lay)
     return _positions(idx)
+
+
+def _items(P, layout):
+    """Pool items of a committee tensor: no more than these can be selected
+    (the ops outputs hold q slots; argsort[::-1][:q] returns min(q, N))."""
+    return P.shape[1] if layout == "MNC" else P.shape[0]
 
 
 class ConsensusEntropySelector:

@@ -51,8 +51,8 @@ class SelectionSession:
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}, got {mode!r}")
         self.q = int(queries)
-        if not 1 <= self.q <= 64:
-            raise ValueError("a session selects 1..64 queries per epoch")
+        if self.q < 0:  # any other q, as the reference's -q (amg_test.py:547-553)
+            raise ValueError(f"queries = {self.q} is negative")
         self.mode = mode
         self.N = int(n_items)
         self.dev = _device(device)
@@ -93,15 +93,21 @@ class SelectionSession:
     def remaining(self):
         return self.N - self.n_selected
 
-    def _mc(self, committee, layout):
+    def _mc(self, committee, layout, q):
         P, lay = stack_committee(committee, self.dev, layout)
         n = P.shape[1] if lay == "MNC" else P.shape[0]
         if n != self.N:
             raise ValueError(f"committee covers {n} items, the session's pool has {self.N}")
-        return ops.select_mc(P, self.q, lay, excl=self.excl)
+        return ops.select_mc(P, q, lay, excl=self.excl)
 
-    def _hc(self, excl=None):
-        return ops.select_mc(self.H.unsqueeze(1), self.q, "NMC", excl=self.excl if excl is None else excl)
+    def _hc(self, q, excl=None):
+        return ops.select_mc(self.H.unsqueeze(1), q, "NMC", excl=self.excl if excl is None else excl)
+
+    def _slots(self):
+        """Output slots per part: q, but never more than the pools hold (argsort
+        [::-1][:q] returns min(q, N)), so a huge q costs no huge buffers."""
+        n = self.N + (self.Nh if self.mode == "mix" else 0)
+        return min(self.q, n)
 
     def select(self, committee=None, layout="MNC"):
         """One epoch: returns the q picked positions (np.int64; fewer when the
@@ -115,21 +121,22 @@ class SelectionSession:
             ops.mark_selected(self.excl, self.N, torch.from_numpy(pick).to(self.dev))
             self.n_selected += len(pick)
             return pick
+        qs = self._slots()
         if self.mode == "mc":
             if committee is None:
                 raise ValueError("mc mode needs `committee`")
-            _, idx = self._mc(committee, layout)
+            _, idx = self._mc(committee, layout, qs)
             ops.mark_selected(self.excl, self.N, idx)
         elif self.mode == "hc":
-            _, idx = self._hc()
+            _, idx = self._hc(qs)
             ops.mark_selected(self.excl, self.N, idx)
         else:  # mix: top-q of each part over the remaining songs, then the union's top-q
             if committee is None:
                 raise ValueError("mix mode needs `committee`")
-            vm, im = self._mc(committee, layout)
-            vh, ih = self._hc(self.excl_hc)
+            vm, im = self._mc(committee, layout, qs)
+            vh, ih = self._hc(qs, self.excl_hc)
             ih = torch.where(ih >= 0, ih + self.N, ih)
-            _, idx = ops.topq_merge(torch.cat([vm, vh]), torch.cat([im, ih]), q)
+            _, idx = ops.topq_merge(torch.cat([vm, vh]), torch.cat([im, ih]), qs)
             # a song leaves both pools whichever part picked it (:484, :521-531)
             is_hc = idx >= self.N
             row = (idx - self.N).clamp(0, self.Nh - 1)

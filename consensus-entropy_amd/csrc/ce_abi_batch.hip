@@ -7,6 +7,7 @@ using namespace ce;
 
 // ---- fused mix ---------------------------------------------------------------
 extern "C" size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t q) {
+    if (q > CE_MAX_Q) return sort_ws_bytes((N > 0 ? N : 0) + (N_h > 0 ? N_h : 0));
     return lists_bytes((int64_t)pool_blocks(N) + pool_blocks(N_h), q < 1 ? 1 : q);
 }
 
@@ -18,16 +19,25 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     if (rc) return rc;
     rc = check_q(q);
     if (rc) return rc;
-    if (N_h < 0 || (N_h > 0 && (!hc || ld_hc < C)) || !val_out || !idx_out)
+    if (N_h < 0 || (N_h > 0 && (!hc || ld_hc < C)) || (q > 0 && (!val_out || !idx_out)))
         return fail(CE_EINVAL, "bad hc table / outputs");
-    const int G1 = pool_blocks(N), G2 = pool_blocks(N_h);
-    if (!ws || ws_bytes < lists_bytes((int64_t)G1 + G2, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (!ws || ws_bytes < ce_select_mix_workspace_bytes(N, N_h, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (q == 0) return CE_OK;
     hipStream_t st = (hipStream_t)stream;
+    const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};  // the hc table: a one-member f64 committee [N_h, 1, C]
+    if (q > CE_MAX_Q) {  // entropies of [mc; hc] (positions 0..N-1, N..N+N_h-1), then the sort path
+        const SortWs s = sort_carve(ws, N + N_h);
+        rc = launch_entropy(a, nullptr, s.ent, st);
+        if (!rc) rc = launch_entropy(t, nullptr, s.ent + N, st);
+        if (rc) return rc;
+        sort_select(s, s.ent, N + N_h, 0, nullptr, q, val_out, idx_out, nullptr, st);
+        return check_launch("ce_select_mix");
+    }
+    const int G1 = pool_blocks(N), G2 = pool_blocks(N_h);
     WsLists w = carve(ws, (int64_t)G1 + G2, q);
     if (q <= kStreamMaxQ && N > 0 && N_h > 0 && N <= kSmallPoolItems && N_h <= kSmallPoolItems &&
         C == 4) {
-        // both segments in ONE launch: tiles of either segment, ticketed merge (k_select_tiles)
-        const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
+        // both segments in ONE block (k_select_tiles)
         if (launch_small_mix(a, t, q, val_out, idx_out, st)) return check_launch("ce_select_mix");
     }
     // both segments on the streaming engine when it applies (q <= 64): the hc
@@ -38,7 +48,6 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
         if (rc) return dispatch_err(rc, a);
     }
     WsLists w2{w.c + (size_t)G1 * q, w.ctr};
-    const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};
     if (launch_stream(t, G2, q, N, w2, st)) {
         finish_lists(w, 1, G1 + G2, q, val_out, idx_out, st);
         return check_launch("ce_select_mix");
@@ -72,6 +81,7 @@ static int64_t batched_lists(int64_t total_items, int U, int q) {
 
 extern "C" size_t ce_select_batched_workspace_bytes(int64_t total_items, int32_t U, int32_t q) {
     if (U < 1) U = 1;
+    if (q > CE_MAX_Q) return sort_ws_bytes(total_items);
     if (q < 1) q = 1;
     return lists_bytes(batched_lists(total_items, U, q), q);
 }
@@ -84,12 +94,22 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     if (rc) return rc;
     rc = check_q(q);
     if (rc) return rc;
-    if (U < 1 || !offsets || !val_out || !idx_out) return fail(CE_EINVAL, "bad batched arguments");
+    if (U < 1 || !offsets || (q > 0 && (!val_out || !idx_out))) return fail(CE_EINVAL, "bad batched arguments");
+    if (!ws || ws_bytes < ce_select_batched_workspace_bytes(total_items, U, q))
+        return fail(CE_EWORKSPACE, "workspace too small");
+    if (q == 0) return CE_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (q > CE_MAX_Q) {  // every user's items contiguous in the total order: sort by (user, key, position)
+        if (U >= kSortMaxUsers) return fail(CE_EUNSUPPORTED, "q > %d needs U < %d users", CE_MAX_Q, kSortMaxUsers);
+        const SortWs s = sort_carve(ws, total_items);
+        rc = launch_entropy(a, nullptr, s.ent, st);
+        if (rc) return rc;
+        sort_keys_users(s.ent, total_items, offsets, U, s.a, st);
+        sort_out_users(sort_run(s, user_sort_passes(U), st), offsets, U, q, val_out, idx_out, st);
+        return check_launch("ce_select_batched");
+    }
     const int bpu = batched_bpu(total_items, U);
     const int64_t nl = (int64_t)bpu * U;
-    if (!ws || ws_bytes < lists_bytes(batched_lists(total_items, U, q), q))
-        return fail(CE_EWORKSPACE, "workspace too small");
-    hipStream_t st = (hipStream_t)stream;
     WsLists w = carve(ws, nl, q);
     if (q <= kStreamMaxQ) {
         // one block per user (k_select_tiles; a user longer than its block streams inside it)

@@ -65,6 +65,27 @@ extern "C" const char* ce_last_error(void) { return g_err; }
 extern "C" const char* ce_version(void) { return "ce_amd 0.1 gfx950"; }
 
 
+int launch_entropy(const CommArgs& a, double* mean_or_null, double* ent, hipStream_t st) {
+    const int64_t N = a.N;
+    if (N == 0) return CE_OK;
+    const int grid = (int)std::min<int64_t>(cdiv(N, kBS), 4096);
+    int rc = with_committee(a, [&](auto src) {
+        hipLaunchKernelGGL((k_entropy<decltype(src)>), dim3(grid), dim3(kBS), 0, st, src, N, mean_or_null, ent);
+    });
+    if (rc == CE_EUNSUPPORTED) {
+        const WideArgs wa = wide_args(a);
+        const PwPlan pl = pw_plan(a.C);
+        const size_t lds = wide_lds_bytes(a.C);
+        const int wgrid = (int)std::min<int64_t>(cdiv(N, 4), 8192);
+        if (mean_or_null) return fail(CE_EUNSUPPORTED, "mean output for C=%d is not implemented", a.C);
+        rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
+            hipLaunchKernelGGL((k_wide_entropy_v<decltype(dt)::value, decltype(npl)::value, decltype(vec)::value>),
+                               dim3(wgrid), dim3(256), lds, st, wa, pl, ent);
+        });
+    }
+    return rc ? dispatch_err(rc, a) : CE_OK;
+}
+
 extern "C" int ce_committee_entropy(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
                                     int64_t sM, int64_t sC, double* mean_or_null, double* ent,
                                     ce_stream_t stream) {
@@ -73,23 +94,8 @@ extern "C" int ce_committee_entropy(const void* p, ce_dtype dt, int64_t N, int32
     if (rc) return rc;
     if (!ent) return fail(CE_EINVAL, "null ent");
     if (N == 0) return CE_OK;
-    hipStream_t st = (hipStream_t)stream;
-    const int grid = (int)std::min<int64_t>(cdiv(N, kBS), 4096);
-    rc = with_committee(a, [&](auto src) {
-        hipLaunchKernelGGL((k_entropy<decltype(src)>), dim3(grid), dim3(kBS), 0, st, src, N, mean_or_null, ent);
-    });
-    if (rc == CE_EUNSUPPORTED) {
-        const WideArgs wa = wide_args(a);
-        const PwPlan pl = pw_plan(C);
-        const size_t lds = wide_lds_bytes(C);
-        const int wgrid = (int)std::min<int64_t>(cdiv(N, 4), 8192);
-        if (mean_or_null) return fail(CE_EUNSUPPORTED, "mean output for C=%d is not implemented", C);
-        rc = with_wide_v(a, [&](auto dt, auto npl, auto vec) {
-            hipLaunchKernelGGL((k_wide_entropy_v<decltype(dt)::value, decltype(npl)::value, decltype(vec)::value>),
-                               dim3(wgrid), dim3(256), lds, st, wa, pl, ent);
-        });
-    }
-    if (rc) return dispatch_err(rc, a);
+    rc = launch_entropy(a, mean_or_null, ent, (hipStream_t)stream);
+    if (rc) return rc;
     return check_launch("ce_committee_entropy");
 }
 
@@ -254,6 +260,7 @@ extern "C" int ce_sgd_predict_proba(const double* X, int64_t F, int32_t D, int64
 
 // ---- top-q of an entropy vector -------------------------------------------
 extern "C" size_t ce_topq_workspace_bytes(int64_t N, int32_t q) {
+    if (q > CE_MAX_Q) return sort_ws_bytes(N);
     return lists_bytes(pool_blocks(N), q < 1 ? 1 : q);
 }
 
@@ -262,10 +269,15 @@ extern "C" int ce_topq(const double* ent, int64_t N, int32_t q, int64_t base_idx
                        double* val_out, int64_t* idx_out, ce_stream_t stream) {
     int rc = check_q(q);
     if (rc) return rc;
-    if (N < 0 || !val_out || !idx_out || (N > 0 && !ent)) return fail(CE_EINVAL, "bad topq arguments");
-    const int G = pool_blocks(N);
-    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (N < 0 || (q > 0 && (!val_out || !idx_out)) || (N > 0 && !ent)) return fail(CE_EINVAL, "bad topq arguments");
+    if (q == 0) return CE_OK;
+    if (!ws || ws_bytes < ce_topq_workspace_bytes(N, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
+    if (q > CE_MAX_Q) {
+        sort_select(sort_carve(ws, N), ent, N, base_idx, nullptr, q, val_out, idx_out, nullptr, st);
+        return check_launch("ce_topq");
+    }
+    const int G = pool_blocks(N);
     WsLists w = carve(ws, G, q);
     Seg sg{nullptr, N, G, base_idx};
     partial_entropies(ent, sg, G, q, w, val_out, idx_out, G == 1, st);
@@ -277,8 +289,11 @@ extern "C" int ce_topq_merge(const double* vals, const int64_t* idx, int32_t nli
                              int64_t* idx_out, ce_stream_t stream) {
     int rc = check_q(q);
     if (rc) return rc;
+    if (q == 0) return CE_OK;
     if (nlists < 1 || !vals || !idx || !val_out || !idx_out) return fail(CE_EINVAL, "bad merge arguments");
-    launch_finish_vals(vals, idx, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
+    if (q > CE_MAX_Q)  // no workspace here: the lists merge by rank (binary searches)
+        rank_merge_lists(nullptr, vals, idx, nlists, q, val_out, idx_out, nullptr, (hipStream_t)stream);
+    else
+        launch_finish_vals(vals, idx, 1, nlists, q, val_out, idx_out, (hipStream_t)stream);
     return check_launch("ce_topq_merge");
 }
-

@@ -5,8 +5,12 @@
 
 using namespace ce;
 
+// q <= 64: the streaming kernels' lists; 64 < q <= CE_MAX_Q: the lists of the
+// entropy vector's selection + the N entropies behind them; q > CE_MAX_Q: the sort path.
 extern "C" size_t ce_select_frames_workspace_bytes(int64_t N, int32_t q) {
-    return lists_bytes(pool_blocks(N), q < 1 ? 1 : q);
+    if (q > CE_MAX_Q) return sort_ws_bytes(N);
+    const size_t lists = lists_bytes(pool_blocks(N), q < 1 ? 1 : q);
+    return q > kStreamMaxQ ? lists + 256 + (size_t)(N > 0 ? N : 0) * 8 : lists;
 }
 
 extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, const int64_t* offsets,
@@ -14,12 +18,12 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
                                 size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
     int rc = check_q(q);
     if (rc) return rc;
-    if (q > kStreamMaxQ) return fail(CE_EUNSUPPORTED, "frame selection needs q <= %d (got %d)", kStreamMaxQ, q);
     if (!members || M < 1 || M > kMaxFrameMembers) return fail(CE_EINVAL, "need 1..%d members (got %d)", kMaxFrameMembers, M);
-    if (N < 0 || (N > 0 && !offsets) || !val_out || !idx_out) return fail(CE_EINVAL, "bad frame selection arguments");
+    if (N < 0 || (N > 0 && !offsets) || (q > 0 && (!val_out || !idx_out)))
+        return fail(CE_EINVAL, "bad frame selection arguments");
     if (C != 2 && C != 3 && C != 4 && C != 8) return fail(CE_EUNSUPPORTED, "frame selection: C=%d not in {2, 3, 4, 8}", C);
     const int G = pool_blocks(N);
-    if (!ws || ws_bytes < lists_bytes(G, q)) return fail(CE_EWORKSPACE, "workspace too small");
+    if (!ws || ws_bytes < ce_select_frames_workspace_bytes(N, q)) return fail(CE_EWORKSPACE, "workspace too small");
     FrameArgs fa{};
     for (int m = 0; m < M; ++m) {
         const ce_member& x = members[m];
@@ -40,6 +44,35 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     fa.base_idx = base_idx;
     fa.nlists = G;
     hipStream_t st = (hipStream_t)stream;
+    if (q == 0) return CE_OK;
+    if (q > kStreamMaxQ) {  // per-song entropies to HBM, then the lists (q <= CE_MAX_Q) or the sort path
+        double* ent;
+        SortWs s{};
+        if (q > CE_MAX_Q) {
+            s = sort_carve(ws, N);
+            ent = s.ent;
+        } else {
+            const WsLists wl = carve(ws, G, q);
+            ent = reinterpret_cast<double*>(((uintptr_t)(wl.c + (int64_t)G * q) + 255) & ~(uintptr_t)255);
+        }
+        if (N > 0) {
+            const int eg = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(N, 256), 8192));
+            switch (C) {
+#define CE_FE(CC) case CC: hipLaunchKernelGGL((k_frames_entropy<CC>), dim3(eg), dim3(256), 0, st, fa, ent); break;
+                CE_FE(2) CE_FE(3) CE_FE(4) CE_FE(8)
+#undef CE_FE
+            }
+        }
+        if (q > CE_MAX_Q) {
+            sort_select(s, ent, N, base_idx, nullptr, q, val_out, idx_out, nullptr, st);
+        } else {
+            WsLists w = carve(ws, G, q);
+            Seg sg{nullptr, N, G, base_idx};
+            partial_entropies(ent, sg, G, q, w, val_out, idx_out, G == 1, st);
+            if (G > 1) finish_lists(w, 1, G, q, val_out, idx_out, st);
+        }
+        return check_launch("ce_select_frames");
+    }
     WsLists w = carve(ws, G, q);
     fa.ctr = w.ctr;
     fa.oval = val_out;

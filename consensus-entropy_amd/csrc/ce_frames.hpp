@@ -169,6 +169,24 @@ __global__ __launch_bounds__(256) void k_frames_select(FrameArgs a, int q, Cand*
     if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm);
 }
 
+// Per-song committee entropy to HBM (k_frames_select's arithmetic, lane per
+// song): the input of the list (64 < q <= CE_MAX_Q) and sort (q > CE_MAX_Q)
+// selections of ce_select_frames.
+template <int C>
+__global__ __launch_bounds__(256) void k_frames_entropy(FrameArgs a, double* __restrict__ ent) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < a.N; n += (int64_t)gridDim.x * 256) {
+        double acc[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = 0.0;  // np.add.reduce identity
+        for (int mm = 0; mm < a.M; ++mm) add_member_mean<C, 8>(a.mem[mm], a, n, true, acc);
+        double mean[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) mean[c] = div_members(acc[c], a.dM, a.invM, a.pow2);
+        ent[n] = entropy_row<C>(mean);
+    }
+}
+
 // The same selection with C lanes per song (lane = (song, class), 64 / C songs
 // per wave step): each lane keeps ONE class's sequential group sum, so the
 // frame rows of the wave's songs are read as whole rows.  Grouped frames (no

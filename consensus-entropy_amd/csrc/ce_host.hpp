@@ -14,6 +14,7 @@
 #include "../../include/ce.h"
 #include "ce_abi.hpp"
 #include "ce_kernels.hpp"
+#include "ce_sort.hpp"
 
 using namespace ce;
 
@@ -56,8 +57,11 @@ static inline WsLists carve(void* ws, int64_t nlists, int q) {
     return w;
 }
 
+// Any q >= 0, as the reference's -q (amg_test.py:547-553): argsort[::-1][:q]
+// returns min(q, N) positions, none for q = 0.  q <= CE_MAX_Q runs on the list
+// kernels; above it on the sort path (ce_sort.hpp, its workspace grows with N).
 static inline int check_q(int q) {
-    if (q < 1 || q > CE_MAX_Q) return fail(CE_EINVAL, "q=%d outside [1, %d]", q, CE_MAX_Q);
+    if (q < 0) return fail(CE_EINVAL, "q=%d is negative", q);
     return CE_OK;
 }
 
@@ -274,6 +278,35 @@ CE_HIDDEN bool launch_small_mix(const CommArgs& a, const CommArgs& t, int q, dou
 CE_HIDDEN bool launch_seg(const CommArgs& a, const int64_t* offsets, int64_t n, int64_t base_idx, int q, int nblocks,
                           int bpu, int threads, double* oval, int64_t* oidx, Cand* wc, const uint32_t* excl,
                           hipStream_t st);
+
+// ce_launch_sort.hip: the sort path for q > CE_MAX_Q (ce_sort.hpp).  Workspace:
+// the 64 KiB header, then n entropies, two n-record buffers, the digit counts
+// and `extra_cands` records.
+CE_HIDDEN size_t sort_ws_bytes(int64_t n, int64_t extra_cands = 0);
+CE_HIDDEN SortWs sort_carve(void* ws, int64_t n, int64_t extra_cands = 0);
+// records {order key (0 if excluded), idx0 + i} of ent[0..n) into out
+CE_HIDDEN void sort_keys(const double* ent, int64_t n, int64_t idx0, const uint32_t* excl, Cand* out, hipStream_t st);
+CE_HIDDEN void sort_keys_users(const double* ent, int64_t n, const int64_t* offsets, int U, Cand* out, hipStream_t st);
+// sorts s.a[0..s.g.n) (generated in ascending position) by key descending, then
+// user_passes passes over the user bits; returns the buffer holding the result
+CE_HIDDEN const Cand* sort_run(const SortWs& s, int user_passes, hipStream_t st);
+CE_HIDDEN int user_sort_passes(int U);
+// the first q slots of sorted records as (val, idx) or records (ocand)
+CE_HIDDEN void sort_out(const Cand* s, int64_t n, int64_t q, double* oval, int64_t* oidx, Cand* ocand, hipStream_t st);
+CE_HIDDEN void sort_out_users(const Cand* s, const int64_t* offsets, int U, int64_t q, double* oval, int64_t* oidx,
+                              hipStream_t st);
+// merge of nl best-first lists of q slots (records c, or (vals, idx)) by rank
+CE_HIDDEN void rank_merge_lists(const Cand* c, const double* vals, const int64_t* idx, int nl, int64_t q, double* oval,
+                                int64_t* oidx, Cand* ocand, hipStream_t st);
+// ce_abi_core.hip: per-item committee entropy (and optional mean) to HBM, any supported shape
+CE_HIDDEN int launch_entropy(const CommArgs& a, double* mean_or_null, double* ent, hipStream_t st);
+
+// entropies ent[0..n) -> the first q slots of the total order (sort path)
+static inline void sort_select(const SortWs& s, const double* ent, int64_t n, int64_t idx0, const uint32_t* excl,
+                               int64_t q, double* oval, int64_t* oidx, Cand* ocand, hipStream_t st) {
+    sort_keys(ent, n, idx0, excl, s.a, st);
+    sort_out(sort_run(s, 0, st), n, q, oval, oidx, ocand, st);
+}
 
 static inline int finish_lists(WsLists w, int segments, int nl, int q, double* val_out, int64_t* idx_out,
                                hipStream_t st) {

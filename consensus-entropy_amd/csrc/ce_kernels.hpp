@@ -189,6 +189,7 @@ struct Seg {
     int64_t N;
     int bpu;
     int64_t base_idx;
+    const uint32_t* excl;    // exclusion bitmap over items 0..N-1 (one segment), or nullptr
 };
 
 __device__ __forceinline__ void seg_range(const Seg& sg, int64_t& s0, int64_t& lo, int64_t& hi) {
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(kBS) void k_partial(Src src, Seg sg, int q, Cand* _
     const int64_t rel = sg.base_idx - s0;
     for (int64_t i0 = lo; i0 < hi; i0 += kBS) {
         const int64_t i = i0 + threadIdx.x;
-        const bool valid = i < hi;
+        const bool valid = i < hi && !(sg.excl && excluded(sg.excl, i));
         uint64_t k = 0;
         if (valid) k = src.key(i);
         tq.offer(k, i + rel, valid);
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(kBS) void k_partial_wide(WideArgs a, PwPlan pl, Seg
             if (lane == j) mykey = order_key(h);
         }
         const int64_t i = i0 + threadIdx.x;
-        tq.offer(mykey, i + rel, i < hi);
+        tq.offer(mykey, i + rel, i < hi && !(sg.excl && excluded(sg.excl, i)));
         tq.end_round(q, kBS);
     }
     const int cnt = tq.finish(q);
@@ -462,9 +463,11 @@ __device__ __forceinline__ void wave_best(uint64_t& k, int64_t& i) {
     }
 }
 
+// ocand != nullptr: the top-q as candidate records instead of (val, idx).
 template <bool FROM_VALS, int CAP, int BS, int IPT>
 __global__ __launch_bounds__(BS) void k_finish(ListSrc<FROM_VALS> src, int nl, int q,
-                                               double* __restrict__ oval, int64_t* __restrict__ oidx) {
+                                               double* __restrict__ oval, int64_t* __restrict__ oidx,
+                                               Cand* __restrict__ ocand) {
     __shared__ TopQSmem<CAP> sm;
     __shared__ uint64_t wk[BS / 64];
     __shared__ int64_t wi[BS / 64];
@@ -520,7 +523,9 @@ __global__ __launch_bounds__(BS) void k_finish(ListSrc<FROM_VALS> src, int nl, i
         }
     }
     const int cnt = tq.finish(q);
-    write_list<CAP, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    if (ocand) write_list<CAP, false>(sm, cnt, q, ocand + slot, nullptr, nullptr);
+    else write_list<CAP, true>(sm, cnt, q, nullptr, oval + slot, oidx + slot);
 }
 
 // Stage 2 for q <= kHeadsMaxQ (the common case, q = 10).  The lists are
@@ -534,7 +539,8 @@ constexpr int kHeadsMaxQ = 512;
 
 template <bool FROM_VALS, int IPT>
 __global__ __launch_bounds__(kHeadsBS) void k_finish_heads(ListSrc<FROM_VALS> src, int nl, int q,
-                                                           double* __restrict__ oval, int64_t* __restrict__ oidx) {
+                                                           double* __restrict__ oval, int64_t* __restrict__ oidx,
+                                                           Cand* __restrict__ ocand) {
     __shared__ TopQSmem<2048> sm;
     const int64_t seg0 = (int64_t)blockIdx.x * nl * q;
     const int64_t L = (int64_t)nl * q;
@@ -616,7 +622,9 @@ __global__ __launch_bounds__(kHeadsBS) void k_finish_heads(ListSrc<FROM_VALS> sr
         }
     }
     const int cnt = tq.finish(q);
-    write_list<2048, true>(sm, cnt, q, nullptr, oval + (int64_t)blockIdx.x * q, oidx + (int64_t)blockIdx.x * q);
+    const int64_t slot = (int64_t)blockIdx.x * q;
+    if (ocand) write_list<2048, false>(sm, cnt, q, ocand + slot, nullptr, nullptr);
+    else write_list<2048, true>(sm, cnt, q, nullptr, oval + slot, oidx + slot);
 }
 
 // Stage 2 for q <= 64.  The lists are best-first, so a list's head is its

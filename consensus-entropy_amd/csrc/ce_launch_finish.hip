@@ -6,7 +6,7 @@
 
 using namespace ce;
 
-// ocand != nullptr: write candidate records (q <= kStreamMaxQ only) instead of (val, idx).
+// ocand != nullptr: write candidate records instead of (val, idx).
 template <bool FROM_VALS>
 static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, double* oval, int64_t* oidx,
                           hipStream_t st, Cand* ocand = nullptr) {
@@ -18,18 +18,18 @@ static void launch_finish(ListSrc<FROM_VALS> src, int segments, int nl, int q, d
     }
     if (q <= kHeadsMaxQ && L > 256) {
         hipLaunchKernelGGL((k_finish_heads<FROM_VALS, 10>), dim3(segments), dim3(kHeadsBS), 0, st, src, nl, q, oval,
-                           oidx);
+                           oidx, ocand);
         return;
     }
     if (L <= 256 && q <= 128)
         hipLaunchKernelGGL((k_finish<FROM_VALS, 512, 256, 1>), dim3(segments), dim3(256), 0, st, src, nl, q, oval,
-                           oidx);
+                           oidx, ocand);
     else if (L <= 4096 && q <= 512)
         hipLaunchKernelGGL((k_finish<FROM_VALS, 2048, 256, 16>), dim3(segments), dim3(256), 0, st, src, nl, q, oval,
-                           oidx);
+                           oidx, ocand);
     else
         hipLaunchKernelGGL((k_finish<FROM_VALS, 4096, kFinBS, 16>), dim3(segments), dim3(kFinBS), 0, st, src, nl,
-                           q, oval, oidx);
+                           q, oval, oidx, ocand);
 }
 
 void launch_finish_lists(const Cand* c, int segments, int nl, int q, double* oval, int64_t* oidx, hipStream_t st,
@@ -39,7 +39,7 @@ void launch_finish_lists(const Cand* c, int segments, int nl, int q, double* ova
 
 void launch_finish_vals(const double* vals, const int64_t* idx, int segments, int nl, int q, double* oval,
                         int64_t* oidx, hipStream_t st) {
-    launch_finish(ListSrc<true>{nullptr, vals, idx}, segments, nl, q, oval, oidx, st);
+    launch_finish(ListSrc<true>{nullptr, vals, idx}, segments, nl, q, oval, oidx, st, nullptr);
 }
 
 void launch_merge_wave(const Cand* c, int segs, int nl, int q, double* oval, int64_t* oidx, hipStream_t st) {

@@ -33,7 +33,13 @@
  *     index (the reference's argsort()[::-1] with its unspecified tie order
  *     tightened to lowest-index-first; -0.0 == +0.0).  Selected outputs are q
  *     slots, best first; slots beyond the number of candidates hold idx = -1 and
- *     val = NaN.
+ *     val = NaN;
+ *   - q is any integer >= 0, as the reference's -q (amg_test.py:547-553;
+ *     argsort()[::-1][:q] returns min(q, N) positions, none for q = 0): q = 0
+ *     writes nothing; q <= CE_MAX_Q runs on the list kernels (workspace of a few
+ *     KB-MB); a larger q runs on a device radix sort of the pool's order keys
+ *     (ce_sort.hpp; its workspace grows with N: ~40 B per item) -- the
+ *     *_workspace_bytes functions size either.
  */
 #ifndef CE_AMD_CE_H
 #define CE_AMD_CE_H
@@ -57,7 +63,7 @@ enum {
     CE_EUNSUPPORTED = -4  /* shape outside what this build implements */
 };
 
-#define CE_MAX_Q 2048
+#define CE_MAX_Q 2048 /* the list kernels' largest q; larger q: the sort path */
 
 const char *ce_last_error(void);
 const char *ce_version(void);
@@ -123,8 +129,8 @@ int ce_segment_mean(const void *frames, ce_dtype dt, int64_t F, int32_t C, int64
  * Every member is f32/f64 [*, C] with row stride ld; a float32 member's song
  * means are rounded to float32 (the groupby result keeps the dtype) and the
  * stack is accumulated in f64 (north star: fp32 load, fp64 accumulate).
- * C in {2, 3, 4, 8}; q <= 64; output as ce_select_mc (positions base_idx + n
- * of the sorted songs).
+ * C in {2, 3, 4, 8}; any q (q <= 64 in one pass; larger q through the per-song
+ * entropies); output as ce_select_mc (positions base_idx + n of the sorted songs).
  */
 typedef struct {
     const void *p;
@@ -212,7 +218,8 @@ int ce_topq(const double *ent, int64_t N, int32_t q, int64_t base_idx, void *ws,
 /*
  * Merge of nlists candidate lists of q slots each (vals/idx: [nlists*q], every
  * list best-first as the ce_* outputs are; idx < 0 = empty slot) into the
- * global top-q.  Used after the RCCL all-gather of per-GPU top-q lists.
+ * global top-q.  Used after the RCCL all-gather of per-GPU top-q lists.  No
+ * workspace: q > CE_MAX_Q merges by rank (a binary search per candidate and list).
  */
 int ce_topq_merge(const double *vals, const int64_t *idx, int32_t nlists, int32_t q,
                   double *val_out, int64_t *idx_out, ce_stream_t stream);
@@ -223,8 +230,8 @@ int ce_topq_merge(const double *vals, const int64_t *idx, int32_t nlists, int32_
  * per-block top-q, then merges the blocks' candidates -- for q <= 64 inside
  * the same launch (the last block to finish merges), so the whole selection
  * is one kernel.
- * ce_select_mc_partial + ce_topq_merge_ws are the same two stages exposed
- * separately (the multi-GPU driver and the bench time them apart).
+ * ce_select_mc_partial + ce_select_finish are the same two stages exposed
+ * separately (q <= CE_MAX_Q; the bench times them apart).
  */
 size_t ce_select_mc_workspace_bytes(int64_t N, int32_t q);
 int ce_select_mc(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
@@ -248,8 +255,8 @@ int ce_select_finish(int64_t N, int32_t q, void *ws, size_t ws_bytes, double *va
  *                           q records to `out` (the all-gather send buffer)
  *   ce_merge_cands          merge nlists such lists (the all-gather receive
  *                           buffer, rank-major) into the final top-q
- * Both need q <= 64 (CE_EUNSUPPORTED otherwise: use ce_select_finish +
- * ce_topq_merge) and 16-byte aligned record buffers.
+ * Any q (ce_select_finish_cands: q <= CE_MAX_Q, a stage 2 of
+ * ce_select_mc_partial) and 16-byte aligned record buffers.
  */
 typedef struct {
     uint64_t key;
@@ -275,7 +282,7 @@ int ce_merge_cands(const ce_cand *c, int32_t nlists, int32_t q, double *val_out,
  * records, best first, 16-byte aligned device memory) in place; first != 0
  * starts a job (running's content is ignored and overwritten).  After the
  * last chunk ce_merge_cands(running, 1, q, ...) returns the selection -- the
- * same as ce_select_mc over the whole pool, ties included.  q <= 64.
+ * same as ce_select_mc over the whole pool, ties included.  Any q.
  */
 size_t ce_select_mc_chunk_workspace_bytes(int64_t N, int32_t q);
 int ce_select_mc_chunk(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
@@ -288,7 +295,8 @@ int ce_select_mc_chunk(const void *p, ce_dtype dt, int64_t N, int32_t M, int32_t
  * rebuilding the pool every epoch, the caller keeps the full pool on the device
  * with an exclusion bitmap (bit i of word i/32 set = item i already queried).
  *   ce_excl_words      uint32 words of a bitmap for N items (host arithmetic)
- *   ce_select_mc_excl  ce_select_mc over the items whose bit is clear (q <= 64)
+ *   ce_select_mc_excl  ce_select_mc over the items whose bit is clear (any q;
+ *                      ws sized by ce_select_mc_workspace_bytes)
  *   ce_mark_selected   set the bits of the n positions idx[0..n) (minus
  *                      base_idx; negative / out-of-range entries ignored) --
  *                      fed the previous call's idx_out, nothing leaves the GPU

@@ -61,8 +61,8 @@ def test_argument_errors_without_gpu():
     from ce_amd import _lib
 
     lib = _lib.load()
-    rc = lib.ce_topq(None, 10, 0, 0, None, 0, None, None, None)  # q = 0
-    assert rc == _lib.CE_EINVAL and b"q=0" in lib.ce_last_error()
+    rc = lib.ce_topq(None, 10, -1, 0, None, 0, None, None, None)  # q < 0
+    assert rc == _lib.CE_EINVAL and b"q=-1" in lib.ce_last_error()
     rc = lib.ce_select_mc(ctypes.c_void_p(16), 0, 10, 0, 4, 4, 4, 1, 10, 0, None, 0, ctypes.c_void_p(16),
                           ctypes.c_void_p(16), None)  # M = 0
     assert rc == _lib.CE_EINVAL

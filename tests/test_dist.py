@@ -94,7 +94,7 @@ def _pool(N, seed):
     return P
 
 
-@pytest.mark.parametrize("world,N,q", [(2, 5000, 10), (2, 7, 10), (3, 4001, 25)])
+@pytest.mark.parametrize("world,N,q", [(2, 5000, 10), (2, 7, 10), (3, 4001, 25), (2, 5000, 65), (3, 3001, 2049)])
 def test_sharded_records_equal_global(world, N, q):
     """The record exchange (ce_cand all-gather, rank-major receive buffer)."""
     mgr = mp.Manager()
@@ -177,7 +177,7 @@ def _worker(rank, world, port, N, q, seed, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,N,q", [(2, 5000, 10), (2, 7, 10), (3, 4001, 25)])
+@pytest.mark.parametrize("world,N,q", [(2, 5000, 10), (2, 7, 10), (3, 4001, 25), (2, 5000, 65)])
 def test_sharded_equals_global(world, N, q):
     mgr = mp.Manager()
     out = mgr.dict()
@@ -256,7 +256,8 @@ def _worker_chunks(rank, world, port, N, chunk, q, seed, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,N,chunk,q", [(2, 9000, 1000, 10), (3, 2500, 1000, 16), (3, 2000, 1000, 10)])
+@pytest.mark.parametrize("world,N,chunk,q", [(2, 9000, 1000, 10), (3, 2500, 1000, 16), (3, 2000, 1000, 10),
+                                             (2, 9000, 1000, 65)])
 def test_sharded_chunks_equal_global(world, N, chunk, q):
     """Pools larger than HBM over several GPUs: chunk c streams on rank
     c % world into that rank's running list; one all-gather of the running
@@ -308,7 +309,7 @@ def _worker_mix(rank, world, port, N, Nh, q, seed, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,N,Nh,q", [(2, 1608, 1608, 10), (3, 500, 97, 16), (2, 5, 3, 10)])
+@pytest.mark.parametrize("world,N,Nh,q", [(2, 1608, 1608, 10), (3, 500, 97, 16), (2, 5, 3, 10), (2, 1608, 1608, 65)])
 def test_sharded_mix_equals_global(world, N, Nh, q):
     """mix (amg_test.py:473-480) sharded over the concatenated [mc; hc] index
     space: the merged answer is the single-process mix, hc positions >= N."""
@@ -364,7 +365,7 @@ def _worker_batched(rank, world, port, U, q, seed, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,U,q", [(2, 37, 10), (3, 8, 5), (3, 2, 10)])
+@pytest.mark.parametrize("world,U,q", [(2, 37, 10), (3, 8, 5), (3, 2, 10), (2, 37, 65)])
 def test_sharded_batched_equals_global(world, U, q):
     """Batched users sharded over ranks, one final gather: every rank holds
     the [U, q] answer of one launch over all users (a rank may hold none)."""

@@ -215,7 +215,9 @@ def test_merge(ce):
 
 def test_errors_are_loud(ce):
     with pytest.raises(ValueError):
-        ce.ops.select_mc(torch.zeros((4, 10, 4), device="cuda"), 0)
+        ce.ops.select_mc(torch.zeros((4, 10, 4), device="cuda"), -1)
+    v, i = ce.ops.select_mc(torch.zeros((4, 10, 4), device="cuda"), 0)  # q = 0: nothing selected
+    assert v.numel() == 0 and i.numel() == 0
     with pytest.raises(ValueError):
         ce.ops.select_mc(torch.zeros((4, 10, 4), device="cuda"), 10, layout="XYZ")
     with pytest.raises(ValueError):
@@ -715,7 +717,7 @@ def test_session_mix_hc_in_own_row_order(ce):
 
 def test_session_rand_and_exhaustion(ce):
     """rand draws only remaining items; a pool smaller than q*epochs runs dry
-    without repeats; the exclusion API rejects q > 64."""
+    without repeats; the exclusion API takes q > 64 too (block lists)."""
     N, q = 45, 10
     sess = ce.SelectionSession(q, "rand", N, rng=np.random.RandomState(1987))
     seen = []
@@ -725,8 +727,9 @@ def test_session_rand_and_exhaustion(ce):
     assert len(sess.select()) == 0
     P = dev(np.full((2, 100, 4), 0.25))
     ex = ce.ops.excl_bitmap(100, "cuda")
-    with pytest.raises(Exception):
-        ce.ops.select_mc(P, 65, excl=ex)
+    ce.ops.mark_selected(ex, 100, torch.arange(0, 100, 2, device="cuda"))
+    _, i = ce.ops.select_mc(P, 65, excl=ex)  # all tied: the 50 odd positions, then padding
+    assert i.cpu().numpy().tolist() == list(range(1, 100, 2)) + [-1] * 15
     sess = ce.SelectionSession(4, "mc", 100)
     for _ in range(25):
         sess.select(committee=P)

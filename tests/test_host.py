@@ -34,10 +34,12 @@ def test_new_entry_points_validate_without_gpu():
     lib = _lib.load()
     p = ctypes.c_void_p(16)
     assert lib.ce_excl_words(0) == 0 and lib.ce_excl_words(33) == 2
-    # q > 64 with an exclusion bitmap / candidate records: unsupported
-    rc = lib.ce_select_mc_excl(p, 0, 100, 4, 4, 16, 4, 1, p, 65, 0, p, 1 << 20, p, p, None)
+    # a negative q is rejected; the two-stage API stops at CE_MAX_Q (ce_select_mc* take any q)
+    rc = lib.ce_select_mc_excl(p, 0, 100, 4, 4, 16, 4, 1, p, -1, 0, p, 1 << 20, p, p, None)
+    assert rc == _lib.CE_EINVAL
+    rc = lib.ce_select_finish_cands(100, _lib.CE_MAX_Q + 1, p, 1 << 20, p, None)
     assert rc == _lib.CE_EUNSUPPORTED
-    rc = lib.ce_select_finish_cands(100, 65, p, 1 << 20, p, None)
+    rc = lib.ce_select_mc_partial(p, 0, 100, 4, 4, 16, 4, 1, _lib.CE_MAX_Q + 1, 0, p, 1 << 20, None)
     assert rc == _lib.CE_EUNSUPPORTED
     rc = lib.ce_select_finish_cands(100, 10, p, 1 << 20, ctypes.c_void_p(24), None)  # misaligned records
     assert rc == _lib.CE_EINVAL
@@ -56,8 +58,8 @@ def test_new_entry_points_validate_without_gpu():
     rc = lib.ce_sgd_predict_proba(p, 10, 260, 260, p, p, 3, 4, p, 4, None)
     assert rc == _lib.CE_EINVAL
     assert lib.ce_mark_selected(None, 10, p, 1, 0, None) == _lib.CE_EINVAL
-    # one-launch records: q > 64 unsupported, misaligned output rejected
-    assert lib.ce_select_mc_cands(p, 0, 100, 4, 4, 16, 4, 1, 65, 0, p, 1 << 20, p, None) == _lib.CE_EUNSUPPORTED
+    # one-launch records: q = 0 writes nothing (no launch), misaligned output rejected
+    assert lib.ce_select_mc_cands(p, 0, 100, 4, 4, 16, 4, 1, 0, 0, p, 1 << 20, None, None) == _lib.CE_OK
     assert lib.ce_select_mc_cands(p, 0, 100, 4, 4, 16, 4, 1, 10, 0, p, 1 << 20, ctypes.c_void_p(24),
                                   None) == _lib.CE_EINVAL
     assert lib.ce_row_div_f64(p, p, -1, p, None) == _lib.CE_EINVAL
@@ -79,7 +81,9 @@ def test_frames_entry_validates_without_gpu():
     assert lib.ce_select_frames(*args(0, 4, 10, ws)) == _lib.CE_EINVAL          # no member
     assert lib.ce_select_frames(*args(33, 4, 10, ws)) == _lib.CE_EINVAL         # too many
     assert lib.ce_select_frames(*args(2, 5, 10, ws)) == _lib.CE_EUNSUPPORTED    # C = 5
-    assert lib.ce_select_frames(*args(2, 4, 65, ws)) == _lib.CE_EUNSUPPORTED    # q > 64
+    assert lib.ce_select_frames(*args(2, 4, -1, ws)) == _lib.CE_EINVAL          # q < 0
+    assert lib.ce_select_frames(*args(2, 4, 65, ws)) == _lib.CE_EWORKSPACE      # q > 64: + the entropies
+    assert lib.ce_select_frames_workspace_bytes(1000, 65) >= ws + 1000 * 8
     assert lib.ce_select_frames(*args(2, 4, 10, 64)) == _lib.CE_EWORKSPACE      # workspace
     bad = (_Member * 1)(_Member(256, 2, 0, 4))                                   # bf16 member
     assert lib.ce_select_frames(*args(1, 4, 10, ws, bad)) == _lib.CE_EUNSUPPORTED
@@ -103,11 +107,45 @@ def test_select_queries_guards_without_gpu():
     from ce_amd import select_queries
     from ce_amd.select import ConsensusEntropySelector
 
-    with pytest.raises(ValueError, match="CE_MAX_Q"):
-        select_queries("mc", 2049, committee=[np.zeros((3, 4))])
+    with pytest.raises(ValueError, match="negative"):
+        select_queries("mc", -1, committee=[np.zeros((3, 4))])
+    assert select_queries("rand", 0, pool=[3, 1, 2]) == []
     with pytest.raises(ValueError, match="mode"):
         ConsensusEntropySelector(10, "qbc")
     sel = ConsensusEntropySelector(10, "mc")
     for empty in (None, [], np.zeros((0, 5, 4))):
         with pytest.raises(ValueError, match="pred_prob"):
             sel.select(pred_prob=empty)
+
+
+def test_any_q_without_gpu():
+    """Any q >= 0 (amg_test.py:547-553): q = 0 returns before any launch on every
+    selecting entry point; q > CE_MAX_Q sizes the sort path's workspace (~40 B
+    per item) and a too small workspace is still rejected on the host."""
+    from ce_amd import _lib
+    from ce_amd.ops import _Member
+
+    lib = _lib.load()
+    p = ctypes.c_void_p(256)
+    big = _lib.CE_MAX_Q + 1
+    N = 1_000_000
+    assert lib.ce_select_mc(p, 0, N, 16, 4, 64, 4, 1, 0, 0, p, 1 << 20, None, None, None) == _lib.CE_OK
+    assert lib.ce_select_mc_excl(p, 0, N, 16, 4, 64, 4, 1, p, 0, 0, p, 1 << 20, None, None, None) == _lib.CE_OK
+    assert lib.ce_topq(p, N, 0, 0, p, 1 << 20, None, None, None) == _lib.CE_OK
+    assert lib.ce_topq_merge(p, p, 4, 0, None, None, None) == _lib.CE_OK
+    assert lib.ce_merge_cands(p, 4, 0, None, None, None) == _lib.CE_OK
+    assert lib.ce_select_mix(p, 0, N, 4, 4, 4, 4 * N, 1, p, 100, 4, 0, p, 1 << 20, None, None, None) == _lib.CE_OK
+    assert lib.ce_select_batched(p, 0, N, 4, 4, 4, 4 * N, 1, p, 10, 0, p, 1 << 20, None, None, None) == _lib.CE_OK
+    assert lib.ce_select_mc_chunk(p, 0, N, 16, 4, 64, 4, 1, 0, 0, None, 1, p, 1 << 20, None) == _lib.CE_OK
+    mem = (_Member * 1)(_Member(256, 0, 0, 4))
+    assert lib.ce_select_frames(ctypes.cast(mem, ctypes.c_void_p), 1, 4, p, None, N, 0, 0, p, 1 << 20, None, None,
+                                None) == _lib.CE_OK
+    for f in (lambda q: lib.ce_select_mc_workspace_bytes(N, q), lambda q: lib.ce_topq_workspace_bytes(N, q),
+              lambda q: lib.ce_select_mix_workspace_bytes(N, 1000, q),
+              lambda q: lib.ce_select_batched_workspace_bytes(N, 500, q),
+              lambda q: lib.ce_select_mc_chunk_workspace_bytes(N, q),
+              lambda q: lib.ce_select_frames_workspace_bytes(N, q)):
+        assert f(big) >= 40 * N > f(10)
+    ws = lib.ce_select_mc_workspace_bytes(N, 10)  # big enough for the lists, not for the sort
+    assert lib.ce_select_mc(p, 0, N, 16, 4, 64, 4, 1, big, 0, p, ws, p, p, None) == _lib.CE_EWORKSPACE
+    assert lib.ce_select_mc(p, 0, N, 16, 4, 64, 4, 1, -5, 0, p, ws, p, p, None) == _lib.CE_EINVAL

@@ -197,3 +197,20 @@ def test_oracle_under_sanitizers():
     r = subprocess.run(["make", "-s", "-C", ORACLE_DIR, "sanitize"], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "sanitized oracle run: ok" in r.stdout
+
+
+def test_full_order_matches_insertion_oracle():
+    """canonical_order (the whole pool in the total order, used for q >
+    CE_MAX_Q where the insertion oracle's O(N q) is too slow) agrees with
+    ce_ref_topq on tie-heavy pools with NaN, -inf, -0.0 / +0.0 and for q beyond N."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(5)
+    for n in (1, 7, 3000):
+        ent = np.floor(rng.random(n) * 16) / 16
+        ent[rng.random(n) < 0.05] = np.nan
+        ent[rng.random(n) < 0.05] = -np.inf
+        ent[rng.random(n) < 0.05] = -0.0
+        ent[rng.random(n) < 0.05] = 0.0
+        for q in (1, n // 2 + 1, n, n + 5):
+            assert np.array_equal(O.canonical_order(ent, q), O.oracle_topq(ent, q)[1]), (n, q)
