@@ -7,7 +7,9 @@ There is no CPU path: a CPU tensor is an error.
 from __future__ import annotations
 
 import ctypes
+import math
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -111,6 +113,18 @@ def log_f64(x):
         raise ValueError("log_f64 takes float64")
     y = torch.empty_like(x)
     call("ce_log_f64", _p(x), x.numel(), _p(y), _stream(x.device))
+    return y
+
+
+def exp_f64(x):
+    """glibc's exp(x) as the engine evaluates it in the GaussianNB member
+    (ce_exp_f64; verification against the C library)."""
+    _on_gpu(x, "x")
+    x = x.contiguous()
+    if x.dtype != torch.float64:
+        raise ValueError("exp_f64 takes float64")
+    y = torch.empty_like(x)
+    call("ce_exp_f64", _p(x), x.numel(), _p(y), _stream(x.device))
     return y
 
 
@@ -277,7 +291,11 @@ def gnb_predict_proba(X, theta, var, class_prior, out=None):
     C = theta.shape[0]
     if tuple(theta.shape) != (C, D) or tuple(var.shape) != (C, D):
         raise ValueError(f"theta/var must be [C, {D}]")
-    log_prior = torch.log(_f64_dev(class_prior, X.device, "class_prior"))  # np.log(class_prior_[i])
+    # np.log(class_prior_[i]) (sklearn 0.24.1 _joint_log_likelihood) with the C
+    # library's log, as numpy 1.19.5 evaluates it: on the host, C values
+    prior = np.asarray(class_prior.cpu() if isinstance(class_prior, torch.Tensor) else class_prior, np.float64)
+    log_prior = torch.tensor([math.log(float(p)) if p > 0 else (-math.inf if p == 0 else math.nan)
+                              for p in prior.reshape(-1)], dtype=torch.float64, device=X.device)
     if out is None:
         out = torch.empty((F, C), dtype=torch.float64, device=X.device)
     call("ce_gnb_predict_proba", _p(X), F, D, X.stride(0), _p(theta), _p(var), _p(log_prior), C, _p(out),

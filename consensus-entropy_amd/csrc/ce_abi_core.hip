@@ -1,6 +1,7 @@
 // ce_abi_core.hip -- C-ABI (include/ce.h): errors, per-item entropy, hc tables,
 // the device log, segment mean, exclusion bitmaps, member inference, top-q and
 // merges.  Kernels: ce_kernels.hpp; dispatch helpers: ce_host.hpp.
+#include "ce_glibc_exp.hpp"
 #include "ce_host.hpp"
 
 using namespace ce;
@@ -10,6 +11,11 @@ namespace ce {
 __global__ __launch_bounds__(kBS) void k_log(const double* __restrict__ x, int64_t n, double* __restrict__ y) {
     stage_log_table();
     for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) y[i] = dlog(x[i]);
+}
+
+// glibc exp over a vector (verification of ce_glibc_exp.hpp against libm).
+__global__ __launch_bounds__(kBS) void k_exp(const double* __restrict__ x, int64_t n, double* __restrict__ y) {
+    for (int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) y[i] = dexp(x[i]);
 }
 
 // x[i] / s[i] through the entropy path's shared-reciprocal division
@@ -106,6 +112,21 @@ extern "C" int ce_log_f64(const double* x, int64_t n, double* y, ce_stream_t str
     const int grid = (int)std::min<int64_t>(cdiv(n, kBS), 8192);
     hipLaunchKernelGGL(k_log, dim3(grid), dim3(kBS), 0, (hipStream_t)stream, x, n, y);
     return check_launch("ce_log_f64");
+}
+
+extern "C" int ce_exp_f64(const double* x, int64_t n, double* y, ce_stream_t stream) {
+    if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad exp arguments");
+    if (n == 0) return CE_OK;
+    const int grid = (int)std::min<int64_t>(cdiv(n, kBS), 8192);
+    hipLaunchKernelGGL(k_exp, dim3(grid), dim3(kBS), 0, (hipStream_t)stream, x, n, y);
+    return check_launch("ce_exp_f64");
+}
+
+extern "C" int ce_exp_f64_host(const double* x, int64_t n, double* y) {
+    if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad exp arguments");
+    const uint64_t* tab = host_exp_table();
+    for (int64_t i = 0; i < n; ++i) y[i] = glibc_exp(x[i], tab);
+    return CE_OK;
 }
 
 extern "C" int ce_row_div_f64(const double* x, const double* s, int64_t n, double* y, ce_stream_t stream) {

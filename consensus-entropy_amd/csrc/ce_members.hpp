@@ -8,10 +8,13 @@
 //     jll_c = log(prior_c) + ((-0.5 * sum_f log(2 pi var_cf)) - 0.5 * sum_f (x_f - theta_cf)^2 / var_cf)
 //     p_c   = exp(jll_c - logsumexp(jll)),  logsumexp = log(sum_c exp(jll_c - max)) + max
 //     Every sum over features is numpy's pairwise sum (np.sum along the row),
-//     reproduced with the same tree as the entropy row sums; only exp / log
-//     (ocml vs glibc, <= 1-2 ulp) differ from the reference.
+//     reproduced with the same tree as the entropy row sums, and exp / log are
+//     glibc's restated (gexp / glog below: numpy 1.19.5 -- the reference's pin
+//     -- calls the C library for float64 exp / log), so predict_proba is the
+//     reference's bit for bit (tests: against the numpy restatement with libm's
+//     exp / log, oracle/ce_oracle.py ref_gnb_predict_proba).
 //   SGDClassifier(loss='log') (_predict_proba_lr): d_k = x . coef_k + b_k,
-//     p_k = expit(d_k) = 1 / (1 + exp(-d_k)), then p /= sum_k p_k (OvR, K > 1),
+//     p_k = expit(d_k) = 1 / (1 + exp(-d_k)) (glibc's exp), then p /= sum_k p_k (OvR, K > 1),
 //     or [1 - p, p] for a binary model.  The dot products are BLAS dgemm in the
 //     reference (an unspecified order); here a fixed wave-reduction order --
 //     parity is to a tolerance (tests state it).
@@ -23,10 +26,18 @@
 // theta / var / coef are staged once per block in LDS.
 #pragma once
 #include "ce_device.hpp"
+#include "ce_glibc_exp.hpp"
 #include "ce_stream.hpp"
 #include "ce_wide.hpp"
 
 namespace ce {
+
+// glibc's f64 exp / log (ce_glibc_exp.hpp, ce_glibc_log.hpp), tables read from
+// global memory (L2-resident): the member kernels stage their own LDS data.
+__device__ __forceinline__ double gexp(double x) { return glibc_exp(x, g_exp_tab); }
+__device__ __forceinline__ double glog(double x) {
+    return glibc_log_fast(x, reinterpret_cast<const LogEntry*>(g_log_tab));
+}
 
 constexpr int kMaxFeat = 512;   // features per frame (the reference: 260)
 constexpr int kMaxMemberC = 8;  // classes (the reference: 4 quadrants)
@@ -171,7 +182,7 @@ __global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
 #pragma unroll
         for (int m = 0; m < NX; ++m) {
             const int f = 8 * m + j;
-            t[m] = f < a.D ? log(2. * M_PI * vr[c * a.D + f]) : 0.0;
+            t[m] = f < a.D ? glog(2. * M_PI * vr[c * a.D + f]) : 0.0;
         }
         const double s1 = group_sum<NX, DF>(t, pl);
         if (gid < a.C && j == 0) hs1[gid] = -0.5 * s1;
@@ -205,12 +216,12 @@ __global__ __launch_bounds__(256) void k_gnb_proba8(GnbArgs a, PwPlan pl) {
         for (int c = 1; c < a.C; ++c) mx = jll[c] > mx ? jll[c] : mx;
         if (!__builtin_isfinite(mx)) mx = 0.0;
         double s = -0.0;
-        for (int c = 0; c < a.C; ++c) s += exp(jll[c] - mx);
-        const double lse = log(0.0 + s) + mx;
+        for (int c = 0; c < a.C; ++c) s += gexp(jll[c] - mx);
+        const double lse = glog(0.0 + s) + mx;
         if (fr < a.F && j < a.C) {
             double v = 0.0;
             for (int c = 0; c < a.C; ++c)
-                if (c == j) v = exp(jll[c] - lse);
+                if (c == j) v = gexp(jll[c] - lse);
             a.out[fr * a.ldo + j] = v;
         }
     }
@@ -253,7 +264,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // 33-log body would set the whole kernel's register budget)
         const int c = g < KC ? g : 0;
         const double* v = vr + c * D + j;
-        auto lg = [&](int m) { return log(2. * M_PI * v[8 * m]); };
+        auto lg = [&](int m) { return glog(2. * M_PI * v[8 * m]); };
         double L[3];
         const int m0[3] = {0, 16, 24}, m1[3] = {16, 24, 32};
 #pragma unroll
@@ -348,17 +359,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         double s = -0.0;
 #pragma unroll
         for (int c = 0; c < KC; ++c) {
-            s += exp(jll[c] - mx);
+            s += gexp(jll[c] - mx);
             asm volatile("" : "+v"(s));
         }
-        const double lse = log(0.0 + s) + mx;
+        const double lse = glog(0.0 + s) + mx;
         const int64_t fr = f0 + g;
         if (fr < a.F && j < a.C) {
             double jl = jll[0];
 #pragma unroll
             for (int c = 1; c < KC; ++c)
                 if (c == j) jl = jll[c];
-            a.out[fr * a.ldo + j] = exp(jl - lse);  // lane j's class only: exp(jll[j] - lse)
+            a.out[fr * a.ldo + j] = gexp(jl - lse);  // lane j's class only: exp(jll[j] - lse)
         }
     }
 }
@@ -369,7 +380,7 @@ __device__ __forceinline__ double sgd_expit(double d, double b) {
     d = d + __shfl_xor(d, 2);
     d = d + __shfl_xor(d, 4);
     d += b;
-    return 1.0 / (1.0 + exp(-d));  // scipy.special.expit
+    return 1.0 / (1.0 + gexp(-d));  // scipy.special.expit
 }
 
 template <int KR>

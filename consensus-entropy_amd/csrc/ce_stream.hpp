@@ -163,6 +163,14 @@ __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t b
     sort_stages<64, 32>(k, i);  // half-cleaners 32 .. 1, all best-first
 }
 
+// no-op callbacks of CommitteeSrc::keys / keys_small (ce_kernels.hpp)
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+struct NoSlot {
+    __device__ __forceinline__ void operator()(int, uint64_t) const {}
+};
+
 // bit i of an exclusion bitmap (SelectionSession: items already queried)
 __device__ __forceinline__ bool excluded(const uint32_t* b, int64_t i) { return (b[i >> 5] >> (i & 31)) & 1u; }
 

@@ -205,6 +205,11 @@ int ce_log_f64(const double *x, int64_t n, double *y, ce_stream_t stream);
  * division (device memory, stream-ordered). */
 int ce_row_div_f64(const double *x, const double *s, int64_t n, double *y, ce_stream_t stream);
 int ce_log_f64_host(const double *x, int64_t n, double *y);
+/* glibc's f64 exp restated (csrc/ce_glibc_exp.hpp; the exp of the GaussianNB
+ * member's logsumexp): device (stream-ordered) and host
+ * (synchronous, no GPU) builds, for verification against the C library. */
+int ce_exp_f64(const double *x, int64_t n, double *y, ce_stream_t stream);
+int ce_exp_f64_host(const double *x, int64_t n, double *y);
 
 /*
  * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]

@@ -382,6 +382,30 @@ int64_t ce_ref_expf_check(const float *got, uint32_t start, int64_t count) {
  * scipy.stats.entropy).  got[i] = an implementation's log(x[i]): how many
  * differ from libm's log bit for bit (NaN matches any NaN).
  * ------------------------------------------------------------------------- */
+/* This libm's exp / log over a vector: numpy 1.19.5 (the reference's pin)
+ * evaluates float64 np.exp / np.log with them; the installed numpy 2.x uses its
+ * own SIMD routines, so the restatements of the members call these instead. */
+void ce_ref_libm_exp(const double *x, int64_t n, double *y) {
+    for (int64_t i = 0; i < n; ++i) y[i] = exp(x[i]);
+}
+void ce_ref_libm_log(const double *x, int64_t n, double *y) {
+    for (int64_t i = 0; i < n; ++i) y[i] = log(x[i]);
+}
+
+/* Mismatches (bit for bit, NaN == NaN) between got[i] and this libm's exp(x[i])
+ * -- the exp numpy 1.19.5 calls for float64 (GaussianNB's logsumexp). */
+int64_t ce_ref_exp_check(const double *x, const double *got, int64_t n) {
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double ref = exp(x[i]);
+        uint64_t a, b;
+        memcpy(&a, &ref, 8);
+        memcpy(&b, &got[i], 8);
+        if (isnan(ref) ? !isnan(got[i]) : a != b) ++bad;
+    }
+    return bad;
+}
+
 int64_t ce_ref_log_check(const double *x, const double *got, int64_t n) {
     int64_t bad = 0;
     for (int64_t i = 0; i < n; ++i) {

@@ -114,28 +114,49 @@ def ref_group_mean(values, s_id):
     return out, keys
 
 
-def ref_gnb_predict_proba(X, theta, var, class_prior):
+def libm_exp(a):
+    """np.exp as numpy 1.19.5 evaluates float64 (the C library's exp, element by
+    element) -- the installed numpy uses its own SIMD exp."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    y = np.empty_like(a)
+    lib().ce_ref_libm_exp(_ptr(a), a.size, _ptr(y))
+    return y
+
+
+def libm_log(a):
+    """np.log as numpy 1.19.5 evaluates float64 (the C library's log)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    y = np.empty_like(a)
+    lib().ce_ref_libm_log(_ptr(a), a.size, _ptr(y))
+    return y
+
+
+def ref_gnb_predict_proba(X, theta, var, class_prior, exp=None, log=None):
     """GaussianNB.predict_proba as the reference's pinned sklearn 0.24.1 +
-    scipy 1.5.4 compute it (amg_test.py:435 on the 'classifier_gnb' member,
-    deam_classifier.py:211): _joint_log_likelihood (np.log of the prior,
-    -0.5 * np.sum(np.log(2 pi var)), -0.5 * np.sum((X - theta)**2 / var, 1)),
-    then predict_log_proba with scipy 1.5.4's logsumexp (amax, non-finite max
-    -> 0, exp, sum, log, + max), then np.exp.  (The installed scipy >= 1.14
-    rewrote logsumexp; tests pin this restatement to the installed sklearn
-    within a stated tolerance.)"""
+    scipy 1.5.4 + numpy 1.19.5 compute it (amg_test.py:435 on the
+    'classifier_gnb' member, deam_classifier.py:211): _joint_log_likelihood
+    (np.log of the prior, -0.5 * np.sum(np.log(2 pi var)), -0.5 *
+    np.sum((X - theta)**2 / var, 1)), then predict_log_proba with scipy 1.5.4's
+    logsumexp (amax, non-finite max -> 0, exp, sum, log, + max), then np.exp.
+    exp / log default to the C library's (libm_exp / libm_log: numpy 1.19.5
+    calls them for float64; the installed numpy's SIMD exp / log differ by an
+    ulp here and there).  The installed scipy >= 1.14 rewrote logsumexp; tests
+    pin this restatement to the installed sklearn within a stated tolerance."""
+    exp = libm_exp if exp is None else exp
+    log = libm_log if log is None else log
     X = np.asarray(X, np.float64)
     jll = []
     for i in range(len(class_prior)):
-        jointi = np.log(class_prior[i])
-        n_ij = -0.5 * np.sum(np.log(2.0 * np.pi * var[i, :]))
+        jointi = log(np.array([class_prior[i]], np.float64))[0]
+        n_ij = -0.5 * np.sum(log(2.0 * np.pi * var[i, :]))
         n_ij -= 0.5 * np.sum(((X - theta[i, :]) ** 2) / (var[i, :]), 1)
         jll.append(jointi + n_ij)
     jll = np.array(jll).T
     a_max = np.amax(jll, axis=1, keepdims=True)
     a_max[~np.isfinite(a_max)] = 0
-    s = np.sum(np.exp(jll - a_max), axis=1)
-    log_prob_x = np.log(s) + np.squeeze(a_max, axis=1)
-    return np.exp(jll - np.atleast_2d(log_prob_x).T)
+    s = np.sum(exp(jll - a_max), axis=1)
+    log_prob_x = log(s) + np.squeeze(a_max, axis=1)
+    return exp(jll - np.atleast_2d(log_prob_x).T)
 
 
 def ref_sgd_predict_proba(X, coef, intercept):
@@ -226,6 +247,8 @@ def lib():
         L.ce_ref_entr.restype = dp
         L.ce_ref_row_sum.argtypes = [vp, i64]
         L.ce_ref_row_sum.restype = dp
+        L.ce_ref_libm_exp.argtypes = [vp, i64, vp]
+        L.ce_ref_libm_log.argtypes = [vp, i64, vp]
         _lib = L
     return _lib
 
@@ -459,6 +482,42 @@ def oracle_log_check(x, got):
     L.ce_ref_log_check.restype = ctypes.c_int64
     L.ce_ref_log_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
     return int(L.ce_ref_log_check(_ptr(x), _ptr(got), x.size))
+
+
+def oracle_exp_check(x, got):
+    """Mismatches (bit for bit, NaN == NaN) between got and libm's exp(x) --
+    the exp numpy 1.19.5 uses for float64 (GaussianNB's logsumexp, §8(f)4)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    got = np.ascontiguousarray(got, dtype=np.float64)
+    assert x.shape == got.shape
+    L = lib()
+    L.ce_ref_exp_check.restype = ctypes.c_int64
+    L.ce_ref_exp_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    return int(L.ce_ref_exp_check(_ptr(x), _ptr(got), x.size))
+
+
+def exp_test_arguments(n, seed):
+    """n f64 arguments covering every branch of glibc's exp: the log-probability
+    range of logsumexp (jll - max <= 0), uniform over the finite range, near 0
+    and tiny (|x| < 2^-54), |x| >= 512 (the rescaled special case, subnormal
+    results included), the overflow / underflow edges, random bit patterns,
+    inf / -inf / NaN / -0."""
+    rng = np.random.default_rng(seed)
+    k = n // 6
+    parts = [
+        -rng.random(k) * 800.0,
+        rng.uniform(-745.2, 709.8, k),
+        rng.standard_normal(k) * 2.0 ** rng.integers(-60, 4, k),
+        rng.uniform(-746.0, -512.0, k // 2),
+        rng.uniform(512.0, 709.8, k // 2),
+        (rng.integers(0, 1 << 63, k, dtype=np.uint64) | (rng.integers(0, 2, k, dtype=np.uint64) << np.uint64(63))).view(np.float64),
+    ]
+    edges = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 709.782712893384, 709.7827128933841, -708.3964185322641,
+                      -744.4400719213812, -745.1332191019411, -745.1332191019412, 512.0, -512.0, 1024.0, -1024.0,
+                      2.0 ** -54, -(2.0 ** -54), 2.0 ** -55, 1.0, -1.0])
+    rest = n - sum(len(p) for p in parts) - len(edges)
+    parts += [edges, rng.uniform(-40.0, 0.0, max(rest, 0))]
+    return np.concatenate(parts)
 
 
 def log_test_arguments(n, seed):

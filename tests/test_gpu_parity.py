@@ -267,6 +267,18 @@ def test_device_log_bit_exact(ce):
     assert bad == 0
 
 
+def test_device_exp_bit_exact(ce):
+    """ce_exp_f64 (glibc's exp restated: the GaussianNB member's logsumexp and
+    expit) against libm's exp on 1e8 arguments covering every branch."""
+    from oracle import ce_oracle as O
+
+    bad = 0
+    for c in range(5):
+        x = O.exp_test_arguments(20_000_000, 200 + c)
+        bad += O.oracle_exp_check(x, ce.ops.exp_f64(dev(x)).cpu().numpy())
+    assert bad == 0
+
+
 def test_row_division_bit_exact(ce):
     """The entropy's row division (one shared reciprocal per row, exact by
     construction -- DESIGN.md 'Numerics') equals IEEE x / s on 6e7 pairs:
@@ -815,18 +827,31 @@ def test_randomised_selection_fuzz(ce):
 
 def test_member_inference_vs_restatement(ce):
     """§8(f)4: GaussianNB / SGD(log) predict_proba on the device against the
-    restatement of the pinned sklearn 0.24.1 + scipy 1.5.4 math.  Tolerance
-    rtol 1e-10: GNB differs only by device vs glibc exp/log (ulps, amplified by
-    |jll| ~ 1e3 at most); SGD's dot products use a fixed wave order, the
-    reference BLAS's."""
+    restatement of the pinned sklearn 0.24.1 + scipy 1.5.4 + numpy 1.19.5 math.
+    GaussianNB: BIT-EXACT (numpy's pairwise sums reproduced, glibc's exp / log
+    restated on the device, the restatement evaluating exp / log with libm as
+    numpy 1.19.5 does) -- both the feature-streamed kernel (D = 260) and the
+    general one (a padded view), a prior of 0 and extreme features included.
+    SGD: rtol 1e-10 (its dot products use a fixed wave order, the reference's
+    BLAS an unspecified one: parity unpinned there)."""
     from conftest import fitted_members
     from oracle.ce_oracle import ref_gnb_predict_proba, ref_sgd_predict_proba
 
     gnb, sgd, Xt = fitted_members(n_test=20_000)
+    Xt = Xt.copy()
+    Xt[::997] *= 40.0  # far from every class: jll ~ -1e4, the logsumexp's shift matters
     Xd = dev(Xt)
+    want = ref_gnb_predict_proba(Xt, gnb.theta_, gnb.var_, gnb.class_prior_)
     got = ce.ops.gnb_predict_proba(Xd, gnb.theta_, gnb.var_, gnb.class_prior_).cpu().numpy()
-    np.testing.assert_allclose(got, ref_gnb_predict_proba(Xt, gnb.theta_, gnb.var_, gnb.class_prior_),
-                               rtol=1e-10, atol=1e-300)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64)), int((got != want).sum())
+    Xpad = torch.zeros((Xt.shape[0], 264), dtype=torch.float64, device="cuda")
+    Xpad[:, :260] = Xd
+    got = ce.ops.gnb_predict_proba(Xpad[:, :260], gnb.theta_, gnb.var_, gnb.class_prior_).cpu().numpy()
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    prior = np.array([0.0, 0.5, 0.25, 0.25])  # a class never seen: log(0) = -inf, p = 0
+    want = ref_gnb_predict_proba(Xt[:3000], gnb.theta_, gnb.var_, prior)
+    got = ce.ops.gnb_predict_proba(Xd[:3000], gnb.theta_, gnb.var_, prior).cpu().numpy()
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
     got = ce.ops.sgd_predict_proba(Xd, sgd.coef_, sgd.intercept_).cpu().numpy()
     np.testing.assert_allclose(got, ref_sgd_predict_proba(Xt, sgd.coef_, sgd.intercept_), rtol=1e-10, atol=1e-300)
     # a binary SGD model: [1 - p, p]

@@ -9,6 +9,7 @@
 #   PHASE=xgb        the same for the XGB member (tools/bench_configs.py --only 7)
 #   PHASE=mpmc       PMC passes over the member kernels (tools/members_pmc.py)
 #   PHASE=small      kernel traces of the small-pool configs + PMC passes of one (tools/small_probe.py)
+#   PHASE=smallab    small-pool configs under rocprofv3 per library build (LIBS="base reg"), alternating
 #   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
@@ -108,6 +109,18 @@ small)  # single-block / small-pool configs: one kernel trace per config + PMC p
   timeout -s KILL 90 rocprofv3 --pmc TA_TA_BUSY_sum SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/${TAG}pmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_ta.log" 2>&1
   step $? "${TAG}pmc ta"
   fi
+  ;;
+smallab)  # A/B of library builds on the small-pool configs: kernel traces, builds alternating (LIBS="base reg ...")
+  cd /tmp
+  for rep in 1 2; do
+    for lib in ${LIBS:-base}; do
+      if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
+      for c in ${CFGS:-c1 c2hc c2mix c3 c3r}; do
+        CE_AMD_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof/ab_${lib}_${c}_$rep" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $c 200 > "$OUT/ab_${lib}_${c}_$rep.log" 2>&1
+        step $? "ab $lib $c $rep"
+      done
+    done
+  done
   ;;
 debug)  # the whole GPU suite once on the debug build (device bounds checks: make -C consensus-entropy_amd debug)
   CE_AMD_LIB=$ROOT/tools/_diag/libce_amd_debug.so timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest_gpu_debug.log" 2>&1
