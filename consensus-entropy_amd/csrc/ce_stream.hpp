@@ -587,22 +587,24 @@ __device__ __forceinline__ void group_best(uint64_t& k, int64_t& i) {
 //      lists -- and the one of rank q-1 is an exact floor T (q lists hold an
 //      entry >= T, so every global top-q candidate is >= T); none when fewer
 //      than q groups hold a list;
-//   2. the lists whose head is >= T (~q of them) are appended to an LDS
-//      index; their q entries are loaded at once (one per thread), those >= T
-//      appended to a survivor list, and every survivor takes the output slot
-//      of its rank among the survivors.
-// More than 64 * W qualifying-list entries or survivors (floods of ties at
-// T): the register-list merge (merge_lists_block) instead.  Round 2 of this
-// round measured the register-list merge at ~20 us as the last block of the
-// 100M-item grid (sequential per-list loads, sort networks on cold lists).
+//   2. every thread walks the lists it loaded whose head is >= T: a list's
+//      entries >= T are a prefix of it (best-first), read 8 at a time, and
+//      appended to a survivor list; every survivor takes the output slot of
+//      its rank among the survivors.
+// The walk reads only the prefixes (for q = 10 on random data: ~q survivors
+// in ~q lists, one round of loads), so q up to 64 stays on this path (round 3
+// loaded every entry of every qualifying list, nq * q, and fell back for any
+// q > 16).  More than 64 * W survivors (floods of ties at T): the
+// register-list merge (merge_lists_block) -- round 2 measured it at ~20 us as
+// the last block of the 100M-item grid (sequential per-list loads, sort
+// networks on cold lists).
 constexpr int kLeanJ = 8;
 template <int W>
 struct LeanMergeSmem {
     uint64_t gk[64];
     int64_t gi[64];
     int part[W][64];
-    int lists[64 * W];
-    int nlists, nsurv, ticket;
+    int nsurv, ticket;
     uint64_t bk[W];
     int64_t bi[W];
 };
@@ -611,6 +613,7 @@ template <int W, class Src>
 __device__ inline void merge_lists_lean(Src src, int nl, int q, WaveListsT<W>& L, LeanMergeSmem<W>& sm,
                                         double* oval, int64_t* oidx, Cand* ocand) {
     constexpr int BS = 64 * W, GS = W;  // lanes per group: 64 groups
+    constexpr int CAP = 64 * W;         // survivors held (the block-merge scratch)
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     uint64_t* sk = &L.key[0][0];  // survivors: the block-merge scratch, 64 W slots
     int64_t* si = &L.idx[0][0];
@@ -639,10 +642,7 @@ __device__ inline void merge_lists_lean(Src src, int nl, int q, WaveListsT<W>& L
         sm.gk[tid / GS] = bk;
         sm.gi[tid / GS] = bi;
     }
-    if (tid == 0) {
-        sm.nlists = 0;
-        sm.nsurv = 0;
-    }
+    if (tid == 0) sm.nsurv = 0;
     __syncthreads();
     {
         const uint64_t mk = sm.gk[lane];
@@ -669,33 +669,37 @@ __device__ inline void merge_lists_lean(Src src, int nl, int q, WaveListsT<W>& L
             fi = sm.gi[sl];
         }
     }
-    // 2. lists whose head is >= T
-#pragma unroll
+    // 2. the prefix >= T of every list whose head is >= T, 8 entries per round
     for (int j = 0; j < kLeanJ; ++j) {
-        if (hi[j] != INT64_MAX && !better(fk, fi, hk[j], hi[j])) {
-            const int s = atomicAdd(&sm.nlists, 1);
-            if (s < BS) sm.lists[s] = tid + BS * j;
-        }
-    }
-    __syncthreads();
-    const int nq = sm.nlists;
-    if (nq * q > BS) {  // block-uniform: floods of ties at T -> the register-list merge
-        merge_lists_block<W>(src, 0, nl, q, L, sm.bk, sm.bi, oval, oidx, ocand);
-        return;
-    }
-    if (tid < nq * q) {
-        const int li = sm.lists[tid / q], e = tid - (tid / q) * q;
-        uint64_t ck;
-        int64_t ci;
-        src.get((int64_t)li * q + e, ck, ci);
-        if (ci >= 0 && !better(fk, fi, ck, ci)) {
-            const int s = atomicAdd(&sm.nsurv, 1);
-            sk[s] = ck;
-            si[s] = ci;
+        if (hi[j] == INT64_MAX || better(fk, fi, hk[j], hi[j])) continue;
+        const int64_t base = (int64_t)(tid + BS * j) * q;
+        for (int e0 = 0; e0 < q; e0 += 8) {
+            uint64_t ck[8];
+            int64_t ci[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) src.get(base + (e0 + u < q ? e0 + u : q - 1), ck[u], ci[u]);  // clamped
+            bool more = true;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (e0 + u >= q || ci[u] < 0 || better(fk, fi, ck[u], ci[u])) {
+                    more = false;
+                    break;
+                }
+                const int s = atomicAdd(&sm.nsurv, 1);
+                if (s < CAP) {
+                    sk[s] = ck[u];
+                    si[s] = ci[u];
+                }
+            }
+            if (!more) break;
         }
     }
     __syncthreads();
     const int ns = sm.nsurv;
+    if (ns > CAP) {  // block-uniform: floods of ties at T -> the register-list merge
+        merge_lists_block<W>(src, 0, nl, q, L, sm.bk, sm.bi, oval, oidx, ocand);
+        return;
+    }
     if (tid < ns) {
         const uint64_t mk = sk[tid];
         const int64_t mi = si[tid];
