@@ -88,33 +88,26 @@ struct CommitteeSrc {
     // item's arithmetic.  Items u >= nlive (wave-
     // uniform: no lane of the wave owns a real item there) skip the arithmetic
     // (key 0).  hook() as in keys().
-    // slot(u, key): called as slot u's key is ready (wave-uniform, u < nlive
-    // only), e.g. to offer it to a per-wave top-q while later slots load.
-    template <int UNR, int IPL, class Hook = NoHook, class Slot = NoSlot, int THR = kSmallThrottle>
+    template <int UNR, int IPL, class Hook = NoHook, int THR = kSmallThrottle>
     __device__ __forceinline__ void keys_small(const int64_t (&items)[IPL], uint64_t (&k)[IPL], int nlive,
-                                               Hook hook = {}, Slot slot = {}) const {
+                                               Hook hook = {}) const {
         if (M > UNR) {
             // committees larger than one batch: f32 rows keep all IPL items' member
             // batches in flight (IPL x UNR x 4 VGPRs); f64 rows of C >= 4 would need
             // twice that, so they go item by item (UNR members in flight)
             if constexpr (!(DT == kF64 && C >= 4)) {
                 keys<UNR, IPL>(items, k, hook);
-#pragma unroll
-                for (int u = 0; u < IPL; ++u)
-                    if (u < nlive) slot(u, k[u]);
                 return;
             }
             int64_t one[1] = {items[0]};
             uint64_t k1[1];
             keys<UNR, 1>(one, k1, hook);
             k[0] = k1[0];
-            if (0 < nlive) slot(0, k[0]);
 #pragma unroll
             for (int u = 1; u < IPL; ++u) {
                 one[0] = items[u];
                 keys<UNR, 1>(one, k1);
                 k[u] = k1[0];
-                if (u < nlive) slot(u, k[u]);
             }
             return;
         }
@@ -158,7 +151,6 @@ struct CommitteeSrc {
 #pragma unroll
                 for (int c = 0; c < C; ++c) m[c] = div_members(acc[c], dM, invM, pow2);
                 k[u] = order_key(entropy_row<C>(m));
-                slot(u, k[u]);
             }
         };
         if (M == UNR) item(std::true_type());

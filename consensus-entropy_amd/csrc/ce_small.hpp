@@ -21,15 +21,6 @@
 
 namespace ce {
 
-// A/B (make variant NAME=reg DEFS=-DCE_SMALL_REG): per-wave register top-q
-// lists fed slot by slot + one rank merge, instead of the block floor +
-// survivor ranking after the last wave
-#ifdef CE_SMALL_REG
-constexpr bool kSmallReg = true;
-#else
-constexpr bool kSmallReg = false;
-#endif
-
 #ifdef CE_PHASE_TIMING
 // diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
 // [0] start, [1] wave 0's keys done, [2] floor, [3] append, [4] rank, [5] merge,
@@ -63,23 +54,17 @@ struct TileSmem {
     int cnt;                                // survivors appended
     uint64_t ck[CAP];
     int64_t ci[CAP];
-    union {
-        WaveListsT<WAVES> lists;            // fallback tree merge
-        Cand wl[WAVES][64];                 // the waves' register lists (kSmallReg)
-    };
-    int nv[WAVES];
+    WaveListsT<WAVES> lists;                // fallback tree merge
 };
 
 // Keys of this thread's IPT items lo + tid + BS*v of [lo, hi) into slots
 // [OFF, OFF + IPT) (all loads in flight before the arithmetic; COMMIT: `tab`
 // is committed once the data is awaited -- exactly one tile_keys call of a
 // block commits).  Slots outside [OFF, OFF + IPT) are left as they are.
-// tq != nullptr: every slot's key is also offered to the wave's register
-// top-q as soon as it is computed (while the next slot's loads are in flight).
 template <class Src, int IPT, int UNR, int BS, int K, int OFF, bool COMMIT>
 __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi, int64_t rel, const uint32_t* excl,
                                           LogTablePrefetch& tab, uint64_t (&k)[K], int64_t (&pos)[K],
-                                          bool (&ok)[K], RegTopQ* tq = nullptr) {
+                                          bool (&ok)[K]) {
     static_assert(OFF + IPT <= K, "");
     const int tid = threadIdx.x, w = tid >> 6;
     const int64_t len = hi - lo;
@@ -96,62 +81,14 @@ __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi
         ok[OFF + v] = j < len;
         if (excl) ok[OFF + v] = ok[OFF + v] && !excluded(excl, items[v]);
     }
-    auto offer = [&](int u, uint64_t key) {
-        if (tq) tq->offer(key, pos[OFF + u], ok[OFF + u]);
-    };
     if (len > 0) {  // block-uniform
-        if constexpr (COMMIT) src.template keys_small<UNR, IPT>(items, kk, nlive, [&]() { tab.commit(); }, offer);
-        else src.template keys_small<UNR, IPT>(items, kk, nlive, NoHook{}, offer);
+        if constexpr (COMMIT) src.template keys_small<UNR, IPT>(items, kk, nlive, [&]() { tab.commit(); });
+        else src.template keys_small<UNR, IPT>(items, kk, nlive);
     } else if constexpr (COMMIT) {
         tab.commit();
     }
 #pragma unroll
     for (int v = 0; v < IPT; ++v) k[OFF + v] = kk[v];
-}
-
-// The block's answer from its waves' exact register top-q lists (q <= 64) in
-// ONE barrier: every wave parks its list in LDS; candidate s of wave w takes
-// output slot s + (entries of every other wave's list that beat it: a binary
-// search, the lists being best-first) -- the items are distinct, so the slots
-// are a permutation; the valid candidates fill slots 0 .. nvalid-1 and the
-// rest is padding.
-template <int W>
-__device__ __forceinline__ void merge_wave_lists_rank(const RegTopQ& tq, Cand (*L)[64], int* nv, int q, double* ov,
-                                                      int64_t* oi) {
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    L[w][lane] = Cand{tq.k, tq.i};
-    const int cnt = __popcll(__ballot(tq.i != INT64_MAX));
-    if (lane == 0) nv[w] = cnt < q ? cnt : q;
-    __syncthreads();
-    int nvalid = 0;
-#pragma unroll
-    for (int v = 0; v < W; ++v) nvalid += nv[v];
-    for (int t = tid; t < W * q; t += 64 * W) {
-        const int a = t / q, sl = t - a * q;
-        const Cand c = L[a][sl];
-        if (c.idx == INT64_MAX) continue;
-        int rank = sl;
-#pragma unroll
-        for (int b = 0; b < W; ++b) {
-            if (b == a) continue;
-            int l = 0, h = q;
-            while (l < h) {
-                const int mid = (l + h) >> 1;
-                const Cand e = L[b][mid];
-                if (better(e.key, e.idx, c.key, c.idx)) l = mid + 1;
-                else h = mid;
-            }
-            rank += l;
-        }
-        if (rank < q) {
-            ov[rank] = key_to_val(c.key);
-            oi[rank] = c.idx;
-        }
-    }
-    for (int r = nvalid + tid; r < q; r += 64 * W) {  // fewer candidates than q: padding
-        ov[r] = __longlong_as_double(0x7ff8000000000000ll);
-        oi[r] = -1;
-    }
 }
 
 // LONG: a problem may exceed BS * IPT items (the per-wave streaming path is
@@ -214,22 +151,6 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
             k[v] = 0;
             pos[v] = INT64_MAX;
             ok[v] = false;
-        }
-        if constexpr (kSmallReg) {
-            // every slot's key goes to the wave's register top-q as it lands; then
-            // one barrier and a rank merge of the W wave lists
-            RegTopQ tq;
-            tq.init(q);
-            tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, rel, excl, tab, k, pos, ok, &tq);
-            if constexpr (IPTB > 0)
-                if (both)
-                    tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, false>(srcB, 0, ta.nB, relB, nullptr, tab, k, pos, ok,
-                                                                    &tq);
-            CE_STAMP(blockIdx.x, 1)
-            CE_WSTAMP(blockIdx.x)
-            merge_wave_lists_rank<W>(tq, sm.wl, sm.nv, q, ov, oi);
-            CE_STAMP(blockIdx.x, 4)
-            return;
         }
         tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, rel, excl, tab, k, pos, ok);
         if constexpr (IPTB > 0)

@@ -163,12 +163,9 @@ __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t b
     sort_stages<64, 32>(k, i);  // half-cleaners 32 .. 1, all best-first
 }
 
-// no-op callbacks of CommitteeSrc::keys / keys_small (ce_kernels.hpp)
+// no-op callback of CommitteeSrc::keys / keys_small (ce_kernels.hpp)
 struct NoHook {
     __device__ __forceinline__ void operator()() const {}
-};
-struct NoSlot {
-    __device__ __forceinline__ void operator()(int, uint64_t) const {}
 };
 
 // bit i of an exclusion bitmap (SelectionSession: items already queried)
@@ -669,29 +666,37 @@ __device__ inline void merge_lists_lean(Src src, int nl, int q, WaveListsT<W>& L
             fi = sm.gi[sl];
         }
     }
-    // 2. the prefix >= T of every list whose head is >= T, 8 entries per round
+    // 2. the prefix >= T of every list whose head is >= T, 8 entries per round.
+    // Rolled, re-reading the head (L2-hot) instead of indexing hk / hi: a runtime
+    // index would put them in scratch, an unrolled walk raises the register
+    // peak of every streaming kernel this merge is inlined into.
+#pragma unroll 1
     for (int j = 0; j < kLeanJ; ++j) {
-        if (hi[j] == INT64_MAX || better(fk, fi, hk[j], hi[j])) continue;
-        const int64_t base = (int64_t)(tid + BS * j) * q;
+        const int g = tid + BS * j;
+        if (g >= nl) break;
+        const int64_t base = (int64_t)g * q;
+        uint64_t h0;
+        int64_t i0;
+        src.get(base, h0, i0);
+        if (i0 < 0 || better(fk, fi, h0, i0)) continue;
+#pragma unroll 1
         for (int e0 = 0; e0 < q; e0 += 8) {
             uint64_t ck[8];
             int64_t ci[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) src.get(base + (e0 + u < q ? e0 + u : q - 1), ck[u], ci[u]);  // clamped
-            bool more = true;
+            int take = 0;  // the leading entries of this round that are >= T
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (e0 + u >= q || ci[u] < 0 || better(fk, fi, ck[u], ci[u])) {
-                    more = false;
-                    break;
+            for (int u = 0; u < 8; ++u)
+                take += (take == u && e0 + u < q && ci[u] >= 0 && !better(fk, fi, ck[u], ci[u])) ? 1 : 0;
+            const int s0 = take ? atomicAdd(&sm.nsurv, take) : 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < take && s0 + u < CAP) {
+                    sk[s0 + u] = ck[u];
+                    si[s0 + u] = ci[u];
                 }
-                const int s = atomicAdd(&sm.nsurv, 1);
-                if (s < CAP) {
-                    sk[s] = ck[u];
-                    si[s] = ci[u];
-                }
-            }
-            if (!more) break;
+            if (take < 8) break;
         }
     }
     __syncthreads();
@@ -760,7 +765,8 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
         lo = ((int64_t)blockIdx.x * 4 + w) * 64;
         hi = a.N;
         step = W * 64;
-    } else {  // the block's 4 waves take alternate tiles of the block's run (adjacent bursts per member row)
+    } else {  // the block's 4 waves take alternate tiles of the block's run (adjacent bursts per member row;
+        // 8 or 64 grid-cyclic sweeps, each over 1/8 or 1/64 of the pool, measured no better: r04_mnc_order.json)
         const int64_t blo = (int64_t)blockIdx.x * 4 * a.per_wave;
         hi = blo + 4 * a.per_wave < a.N ? blo + 4 * a.per_wave : a.N;
         lo = blo + 64 * w;

@@ -9,6 +9,7 @@
 #   PHASE=xgb        the same for the XGB member (tools/bench_configs.py --only 7)
 #   PHASE=mpmc       PMC passes over the member kernels (tools/members_pmc.py)
 #   PHASE=small      kernel traces of the small-pool configs + PMC passes of one (tools/small_probe.py)
+#   PHASE=c5         rocprofv3 of the full C5 job (tools/bench_c5.py) + PMC passes at 12M items
 #   PHASE=smallab    small-pool configs under rocprofv3 per library build (LIBS="base reg"), alternating
 #   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
@@ -109,6 +110,20 @@ small)  # single-block / small-pool configs: one kernel trace per config + PMC p
   timeout -s KILL 90 rocprofv3 --pmc TA_TA_BUSY_sum SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/${TAG}pmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/small_probe.py" $P 20 > "$OUT/${TAG}pmc_ta.log" 2>&1
   step $? "${TAG}pmc ta"
   fi
+  ;;
+c5)  # BASELINE configs[4]: rocprofv3 kernel trace of the full 50M x 32 x 1000 bf16 job + PMC passes on 12M items
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof/c5_job" -o run --output-format csv -- python3 "$ROOT/tools/bench_c5.py" > "$OUT/c5_job.json" 2> "$OUT/c5_job.err"
+  step $? "c5 job trace"
+  A="--items 12000000"
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/c5_fetch" -o run --output-format csv -- python3 "$ROOT/tools/bench_c5.py" $A > "$OUT/c5_fetch.log" 2>&1
+  step $? "c5 fetch"
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/c5_write" -o run --output-format csv -- python3 "$ROOT/tools/bench_c5.py" $A > "$OUT/c5_write.log" 2>&1
+  step $? "c5 write"
+  timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/prof/c5_sq" -o run --output-format csv -- python3 "$ROOT/tools/bench_c5.py" $A > "$OUT/c5_sq.log" 2>&1
+  step $? "c5 sq"
+  timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE -d "$OUT/prof/c5_lds" -o run --output-format csv -- python3 "$ROOT/tools/bench_c5.py" $A > "$OUT/c5_lds.log" 2>&1
+  step $? "c5 lds"
   ;;
 smallab)  # A/B of library builds on the small-pool configs: kernel traces, builds alternating (LIBS="base reg ...")
   cd /tmp
