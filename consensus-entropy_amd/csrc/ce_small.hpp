@@ -6,13 +6,18 @@
 //   1. the log table's loads are issued, then the member loads of the
 //      thread's item slots (item lo + tid + BS*v: each wave's loads coalesced);
 //      each item's mean + entropy runs as soon as its own loads have landed;
-//   2. the best key of each group of BS/64 lanes (lane-exchange butterfly) ->
-//      64 group bests (distinct items) in LDS; every thread ranks one of them
-//      against a 1/W slice of the others; the group best of rank q-1 is an
-//      exact floor (q items are >= it);
+//   2. the max key of each group of BS/64 lanes (DPP mirrors) -> 64 group
+//      items (distinct) in LDS; every thread ranks one of them against a 1/W
+//      slice of the others; the group item of rank q-1 is an exact floor (q
+//      items are >= it);
 //   3. items >= the floor are appended to an LDS list (one atomic per wave);
 //      survivor t counts the survivors that beat it and writes itself to
 //      output slot `rank` (< q).
+// Items are compared as (key, ~local slot) triples -- the local slot v*BS+tid
+// orders a problem's items as their positions do -- with a 96-bit subtract's
+// borrow (add_if_beats), and no position or validity array stays live across
+// the keys phase (round 3's kept one and spilled it to scratch in the batched
+// kernel: the reload sat at the head of the floor phase).
 // A problem longer than BS*IPT items (a long user of a ragged batch), or more
 // than 64*W survivors (floods of exact ties at the floor), takes per-wave
 // register lists + a tree merge instead (block-uniform branches, same answer).
@@ -26,8 +31,12 @@ namespace ce {
 // [0] start, [1] wave 0's keys done, [2] floor, [3] append, [4] rank, [5] merge,
 // [6 + w] wave w's keys done (w < 8)
 __device__ uint64_t g_phase[8192][16];
-#define CE_STAMP(b, k) \
-    if (threadIdx.x == 0 && (b) < 8192) g_phase[b][k] = wall_clock64();
+// [14], [15]: shader-clock counter at [0] and [4] (the clock rate over the block)
+#define CE_STAMP(b, k)                                        \
+    if (threadIdx.x == 0 && (b) < 8192) {                     \
+        g_phase[b][k] = wall_clock64();                       \
+        if ((k) == 0 || (k) == 4) g_phase[b][14 + (k) / 4] = clock64(); \
+    }
 #define CE_WSTAMP(b) \
     if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 8 && (b) < 8192) g_phase[b][6 + (threadIdx.x >> 6)] = wall_clock64();
 #else
@@ -48,23 +57,21 @@ struct TileArgs {
 template <int WAVES>
 struct TileSmem {
     static constexpr int CAP = 64 * WAVES;  // one survivor per thread
-    uint64_t gk[64];                        // group bests
-    int64_t gi[64];
-    int part[WAVES][64];                    // partial ranks of the group bests
+    uint4 gb[64];                           // group items (~local slot, key lo, key hi, -)
+    int part[WAVES][64];                    // partial ranks of the group items
     int cnt;                                // survivors appended
-    uint64_t ck[CAP];
-    int64_t ci[CAP];
+    uint4 cs[CAP];                          // survivors (~local slot, key lo, key hi, -)
     WaveListsT<WAVES> lists;                // fallback tree merge
 };
 
 // Keys of this thread's IPT items lo + tid + BS*v of [lo, hi) into slots
-// [OFF, OFF + IPT) (all loads in flight before the arithmetic; COMMIT: `tab`
-// is committed once the data is awaited -- exactly one tile_keys call of a
-// block commits).  Slots outside [OFF, OFF + IPT) are left as they are.
+// [OFF, OFF + IPT): key 0 for a slot past the end or an excluded item (all
+// loads in flight before the arithmetic; COMMIT: `tab` is committed once the
+// data is awaited -- exactly one tile_keys call of a block commits).  Slots
+// outside [OFF, OFF + IPT) are left as they are.
 template <class Src, int IPT, int UNR, int BS, int K, int OFF, bool COMMIT>
-__device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi, int64_t rel, const uint32_t* excl,
-                                          LogTablePrefetch& tab, uint64_t (&k)[K], int64_t (&pos)[K],
-                                          bool (&ok)[K]) {
+__device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi, const uint32_t* excl,
+                                          LogTablePrefetch& tab, uint64_t (&k)[K]) {
     static_assert(OFF + IPT <= K, "");
     const int tid = threadIdx.x, w = tid >> 6;
     const int64_t len = hi - lo;
@@ -77,9 +84,6 @@ __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi
         items[v] = lo + (j < len ? j : (len > 0 ? len - 1 : 0));
         kk[v] = 0;
         nlive += (int64_t)BS * v + 64 * w < len;
-        pos[OFF + v] = items[v] + rel;
-        ok[OFF + v] = j < len;
-        if (excl) ok[OFF + v] = ok[OFF + v] && !excluded(excl, items[v]);
     }
     if (len > 0) {  // block-uniform
         if constexpr (COMMIT) src.template keys_small<UNR, IPT>(items, kk, nlive, [&]() { tab.commit(); });
@@ -88,7 +92,46 @@ __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi
         tab.commit();
     }
 #pragma unroll
-    for (int v = 0; v < IPT; ++v) k[OFF + v] = kk[v];
+    for (int v = 0; v < IPT; ++v) {
+        bool ok = tid + (int64_t)BS * v < len;
+        if (excl) ok = ok && !excluded(excl, items[v]);
+        k[OFF + v] = ok ? kk[v] : 0ull;
+    }
+}
+
+// r + 1 when triple a beats triple m, (~local slot, key lo, key hi) each: the
+// borrow of the 96-bit difference m - a (higher key first, then lower slot) --
+// three subtracts and an add-with-carry, no compare masks or scalar ops.
+__device__ __forceinline__ int add_if_beats(int r, const uint4& m, const uint4& a) {
+    int out;
+    uint32_t t;
+    asm("v_sub_co_u32 %1, vcc, %2, %5\n\t"
+        "v_subb_co_u32 %1, vcc, %3, %6, vcc\n\t"
+        "v_subb_co_u32 %1, vcc, %4, %7, vcc\n\t"
+        "v_addc_co_u32 %0, vcc, 0, %8, vcc"
+        : "=v"(out), "=&v"(t)
+        : "v"(m.x), "v"(m.y), "v"(m.z), "v"(a.x), "v"(a.y), "v"(a.z), "v"(r)
+        : "vcc");
+    return out;
+}
+
+// The max key of each group of GS lanes (and the slot of one item holding it)
+// in the group's lanes: DPP mirrors within quads, half rows and rows.
+template <int GS>
+__device__ __forceinline__ void group_max(uint64_t& k, uint32_t& n) {
+#define CE_GM(J, CTL)                                                                                  \
+    if constexpr (GS > J) {                                                                            \
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)k, CTL, 0xF, 0xF, false);         \
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(k >> 32), CTL, 0xF, 0xF, false); \
+        const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n, CTL, 0xF, 0xF, false);                   \
+        const uint64_t pk = ((uint64_t)p1 << 32) | p0;                                                 \
+        if (pk > k) {                                                                                  \
+            k = pk;                                                                                    \
+            n = pn;                                                                                    \
+        }                                                                                              \
+    }
+    CE_GM(1, 0xB1) CE_GM(2, 0x4E) CE_GM(4, 0x141) CE_GM(8, 0x140)  // quad [1,0,3,2], [2,3,0,1]; half-row, row mirror
+#undef CE_GM
 }
 
 // LONG: a problem may exceed BS * IPT items (the per-wave streaming path is
@@ -143,61 +186,64 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         return;
     } else {
         // 1. keys of this thread's items
-        uint64_t k[K];
-        int64_t pos[K];
-        bool ok[K];
+        uint64_t kz[K];  // key 0: no item
 #pragma unroll
-        for (int v = 0; v < K; ++v) {
-            k[v] = 0;
-            pos[v] = INT64_MAX;
-            ok[v] = false;
-        }
-        tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, rel, excl, tab, k, pos, ok);
+        for (int v = 0; v < K; ++v) kz[v] = 0;
+        tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, excl, tab, kz);
         if constexpr (IPTB > 0)
-            if (both) tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, false>(srcB, 0, ta.nB, relB, nullptr, tab, k, pos, ok);
+            if (both) tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, false>(srcB, 0, ta.nB, nullptr, tab, kz);
         CE_STAMP(blockIdx.x, 1)
         CE_WSTAMP(blockIdx.x)
-        uint64_t bk = 0;
-        int64_t bi = INT64_MAX;
+        // 2. every slot as a triple (~local slot, key lo, key hi): local slot
+        //    L = v * BS + tid orders the block's items as their positions do,
+        //    so "a beats b" is the 96-bit compare of the triples (key 0: no item)
+        const uint32_t ntid = ~(uint32_t)tid;
+        uint32_t nl[K];
 #pragma unroll
-        for (int v = 0; v < K; ++v)
-            if (ok[v] && better(k[v], pos[v], bk, bi)) {
-                bk = k[v];
-                bi = pos[v];
+        for (int v = 0; v < K; ++v) nl[v] = ntid - (uint32_t)(v * BS);  // ~(v * BS + tid)
+        // the lane's max key, its lowest slot on ties; then the group's max key
+        // (a tie keeps the lane's own item: any item holding the group's max
+        // key stands for the group -- 64 distinct items)
+        uint64_t bk = kz[0];
+        uint32_t bn = nl[0];
+#pragma unroll
+        for (int v = 1; v < K; ++v)
+            if (kz[v] > bk) {
+                bk = kz[v];
+                bn = nl[v];
             }
-        // 2. floor = the group best of rank q-1 (ranks split over the waves)
-        group_best<GS>(bk, bi);
-        if ((tid & (GS - 1)) == 0) {
-            sm.gk[tid / GS] = bk;
-            sm.gi[tid / GS] = bi;
-        }
+        group_max<GS>(bk, bn);
+        if ((tid & (GS - 1)) == 0) sm.gb[tid / GS] = make_uint4(bn, (uint32_t)bk, (uint32_t)(bk >> 32), 0u);
         if (tid == 0) sm.cnt = 0;
         __syncthreads();
+        // floor = the group item of rank q-1 (ranks split over the waves; the
+        // 64 triples are distinct, so exactly one lane holds rank q-1 <= 63)
+        const uint4 mg = sm.gb[lane];
         {
-            const uint64_t mk = sm.gk[lane];
-            const int64_t mi = sm.gi[lane];
             int r = 0;
 #pragma unroll
-            for (int j = 0; j < 64 / W; ++j) {
-                const int o = w * (64 / W) + j;
-                r += better(sm.gk[o], sm.gi[o], mk, mi);
-            }
+            for (int j = 0; j < 64 / W; ++j) r = add_if_beats(r, mg, sm.gb[w * (64 / W) + j]);
             sm.part[w][lane] = r;
         }
         __syncthreads();
-        uint64_t fk = 0;  // no group best of rank q-1 (fewer valid groups): admit every valid item
-        int64_t fi = INT64_MAX;
+        uint64_t fk;
+        uint32_t fn;
         {
             int r = 0;
 #pragma unroll
             for (int j = 0; j < W; ++j) r += sm.part[j][lane];
-            const uint64_t hit = __ballot(r == q - 1);
-            if (hit) {
-                const int sl = __builtin_ctzll(hit);
-                fk = sm.gk[sl];
-                fi = sm.gi[sl];
-            }
+            const int sl = __builtin_ctzll(__ballot(r == q - 1));
+            fn = (uint32_t)__builtin_amdgcn_readlane((int)mg.x, sl);
+            fk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mg.z, sl) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)mg.y, sl);
         }
+        const bool floor = fk != 0;  // else fewer than q groups hold an item: admit every item
+        if (!floor) fn = 0;
+        if (!floor) fk = 1;  // every valid key is > 1, key 0 (no item) is not
+        // position of local slot L (segment A's slots first, then segment B's)
+        auto pos_of = [&](uint32_t L) -> int64_t {
+            return L < (uint32_t)(IPTA * BS) ? lo + rel + (int64_t)L : (int64_t)(L - (uint32_t)(IPTA * BS)) + relB;
+        };
         CE_STAMP(blockIdx.x, 2)
         // 3. survivors (not worse than the floor) -> LDS list: the wave's K
         //    ballots first, then ONE atomic per wave for all of its survivors
@@ -208,7 +254,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
             int tot = 0;
 #pragma unroll
             for (int v = 0; v < K; ++v) {
-                pass[v] = ok[v] && !better(fk, fi, k[v], pos[v]);
+                pass[v] = (kz[v] > fk) | ((kz[v] == fk) & (nl[v] >= fn));  // bitwise: no per-slot branches
                 m[v] = __ballot(pass[v]);
                 tot += __popcll(m[v]);
             }
@@ -220,10 +266,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 for (int v = 0; v < K; ++v) {
                     const int slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[v] >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m[v], 0));
-                    if (pass[v] && slot < SM::CAP) {
-                        sm.ck[slot] = k[v];
-                        sm.ci[slot] = pos[v];
-                    }
+                    if (pass[v] && slot < SM::CAP)
+                        sm.cs[slot] = make_uint4(nl[v], (uint32_t)kz[v], (uint32_t)(kz[v] >> 32), 0u);
                     base += __popcll(m[v]);
                 }
             }
@@ -233,14 +277,13 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         const int nc = sm.cnt;
         if (nc <= SM::CAP) {
             if (tid < nc) {  // survivor tid takes the slot of its rank
-                const uint64_t mk = sm.ck[tid];
-                const int64_t mi = sm.ci[tid];
+                const uint4 me = sm.cs[tid];
                 int r = 0;
-                // (batching 8 LDS reads per step measured slower: rank 0.64 -> 0.80 us)
-                for (int j = 0; j < nc; ++j) r += better(sm.ck[j], sm.ci[j], mk, mi);
+#pragma unroll 8
+                for (int j = 0; j < nc; ++j) r = add_if_beats(r, me, sm.cs[j]);
                 if (r < q) {
-                    ov[r] = key_to_val(mk);
-                    oi[r] = mi;
+                    ov[r] = key_to_val(((uint64_t)me.z << 32) | me.y);
+                    oi[r] = pos_of(~me.x);
                 }
             } else if (tid < q) {  // fewer survivors than q: padding
                 ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
@@ -250,9 +293,10 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         } else {
             // overflow (> CAP items tie at or above the floor): per-wave lists + tree merge
             RegTopQ tq;
-            tq.init(q, fk, fi == INT64_MAX ? fi : fi + 1);  // admit candidates >= the floor
+            if (floor) tq.init(q, fk, pos_of(~fn) + 1);  // admit candidates >= the floor
+            else tq.init(q, 0, INT64_MAX);
 #pragma unroll
-            for (int v = 0; v < K; ++v) tq.offer(k[v], pos[v], ok[v]);
+            for (int v = 0; v < K; ++v) tq.offer(kz[v], pos_of(~nl[v]), kz[v] != 0);
             block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
         }
     }

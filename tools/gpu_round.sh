@@ -142,8 +142,12 @@ debug)  # the whole GPU suite once on the debug build (device bounds checks: mak
   step $? "pytest debug build"
   ;;
 phase)  # per-block phase stamps of the C3 selection (tools/phase_probe.py) on the diagnostic build (make phase)
-  CE_AMD_LIB=$ROOT/tools/_diag/ce_amd_phase.so timeout -k 10 120 python3 tools/phase_probe.py > "$OUT/phase.json" 2> "$OUT/phase.err"
-  step $? "phase probe"
+  for lib in ${PLIBS:-ce_amd_phase}; do  # phase-stamp builds in tools/_diag (make phase / make variant DEFS=-DCE_PHASE_TIMING ...)
+    for c in ${CFGS:-c3 c1}; do
+      CE_AMD_LIB=$ROOT/tools/_diag/$lib.so timeout -k 10 120 python3 tools/phase_probe.py $c > "$OUT/phase_${lib}_$c.json" 2> "$OUT/phase_${lib}_$c.err"
+      step $? "phase probe $lib $c"
+    done
+  done
   ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
