@@ -45,7 +45,7 @@ constexpr int kSegWaves = 16;     // waves per single-block pool / per user (k_s
 // ---------------------------------------------------------------------------
 
 
-// item slots a lane keeps in flight in the single-block pools (keys_small).
+// item slots a lane keeps in flight in the single-block pools (rows_small).
 // Measured on configs[2] (500 users x 1608, f32): all at once 14.24 us,
 // 1 slot 13.52 us, 2 slots 14.68 us
 constexpr int kSmallThrottle = 1;
@@ -77,37 +77,42 @@ struct CommitteeSrc {
 #pragma unroll
         for (int u = 0; u < IPL; ++u) k[u] = order_key(entropy_row<C>(m[u]));
     }
-    // keys() for latency-bound single-block pools: when the whole committee
-    // fits one batch (M <= UNR) the loads are issued item by item and each
-    // item's mean + entropy runs as soon as ITS loads have landed, so only the
-    // last item's arithmetic trails the last load.  Every slot's loads are
-    // issued, also for slots without a real item (their addresses are clamped
-    // to the pool's last item: one cache line per wave): loads under a branch
-    // leave the compiler unable to count them, and it then waits for ALL of
-    // them (vmcnt(0)) before the log table's commit, i.e. before the first
-    // item's arithmetic.  Items u >= nlive (wave-
-    // uniform: no lane of the wave owns a real item there) skip the arithmetic
-    // (key 0).  hook() as in keys().
-    template <int UNR, int IPL, class Hook = NoHook, int THR = kSmallThrottle>
-    __device__ __forceinline__ void keys_small(const int64_t (&items)[IPL], uint64_t (&k)[IPL], int nlive,
+    // The exact consensus rows (amg_test.py:441) of IPL item slots for the
+    // latency-bound single-block pools: sink(u, m) receives slot u's row, for
+    // u < nlive only (wave-uniform: no lane of the wave owns a real item at u
+    // >= nlive).  When the whole committee fits one batch (M <= UNR) the loads
+    // are issued item by item and each item's mean runs as soon as ITS loads
+    // have landed.  Every slot's loads are issued, also for slots without a
+    // real item (their addresses are clamped to the pool's last item: one
+    // cache line per wave): loads under a branch leave the compiler unable to
+    // count them, and it then waits for ALL of them (vmcnt(0)) before the log
+    // table's commit.  hook() runs after the first means (e.g.
+    // LogTablePrefetch::commit).
+    template <int UNR, int IPL, class Sink, class Hook = NoHook, int THR = kSmallThrottle>
+    __device__ __forceinline__ void rows_small(const int64_t (&items)[IPL], int nlive, Sink&& sink,
                                                Hook hook = {}) const {
         if (M > UNR) {
             // committees larger than one batch: f32 rows keep all IPL items' member
             // batches in flight (IPL x UNR x 4 VGPRs); f64 rows of C >= 4 would need
             // twice that, so they go item by item (UNR members in flight)
             if constexpr (!(DT == kF64 && C >= 4)) {
-                keys<UNR, IPL>(items, k, hook);
+                int64_t offs[IPL];
+#pragma unroll
+                for (int u = 0; u < IPL; ++u) offs[u] = items[u] * sN;
+                double m[IPL][C];
+                committee_mean_multi<DT, C, VEC, UNR, IPL>(p, offs, M, sM, sC, dM, invM, pow2, m);
+                hook();
+#pragma unroll
+                for (int u = 0; u < IPL; ++u)
+                    if (u < nlive) sink(u, m[u]);
                 return;
             }
-            int64_t one[1] = {items[0]};
-            uint64_t k1[1];
-            keys<UNR, 1>(one, k1, hook);
-            k[0] = k1[0];
 #pragma unroll
-            for (int u = 1; u < IPL; ++u) {
-                one[0] = items[u];
-                keys<UNR, 1>(one, k1);
-                k[u] = k1[0];
+            for (int u = 0; u < IPL; ++u) {
+                double m[C];
+                committee_mean<DT, C, VEC, UNR>(p, items[u] * sN, M, sM, sC, dM, invM, pow2, m);
+                if (u == 0) hook();
+                if (u < nlive) sink(u, m);
             }
             return;
         }
@@ -139,7 +144,6 @@ struct CommitteeSrc {
                         issue(u + D);
                     }
                 }
-                k[u] = 0;
                 if (u >= nlive) continue;  // wave-uniform
                 double acc[C];
 #pragma unroll
@@ -152,7 +156,7 @@ struct CommitteeSrc {
                 double m[C];
 #pragma unroll
                 for (int c = 0; c < C; ++c) m[c] = div_members(acc[c], dM, invM, pow2);
-                k[u] = order_key(entropy_row<C>(m));
+                sink(u, m);
             }
         };
         if (M == UNR) item(std::true_type());

@@ -5,21 +5,31 @@
 // Per block (amg_test.py:441-445 on the problem's items):
 //   1. the log table's loads are issued, then the member loads of the
 //      thread's item slots (item lo + tid + BS*v: each wave's loads coalesced);
-//      each item's mean + entropy runs as soon as its own loads have landed;
-//   2. the max key of each group of BS/64 lanes (DPP mirrors) -> 64 group
-//      items (distinct) in LDS; every thread ranks one of them against a 1/W
-//      slice of the others; the group item of rank q-1 is an exact floor (q
-//      items are >= it);
-//   3. items >= the floor are appended to an LDS list (one atomic per wave);
-//      survivor t counts the survivors that beat it and writes itself to
-//      output slot `rank` (< q).
-// Items are compared as (key, ~local slot) triples -- the local slot v*BS+tid
-// orders a problem's items as their positions do -- with a 96-bit subtract's
-// borrow (add_if_beats), and no position or validity array stays live across
-// the keys phase (round 3's kept one and spilled it to scratch in the batched
-// kernel: the reload sat at the head of the floor phase).
+//      each item's exact consensus row (f64 means) is formed as soon as its
+//      own loads have landed, and kept in registers; from it an APPROXIMATE
+//      entropy -- f32 copies, one hardware reciprocal, four hardware log2 --
+//      within kApproxErr2 of the exact one (log2 units), a 32-bit key;
+//   2. the max approximate key of each group of BS/64 lanes (DPP) -> 64 group
+//      maxima (distinct items) in LDS; every thread counts, for one of them,
+//      the maxima above / not below it over a 1/W slice; the value T of rank
+//      q-1 has q distinct items at or above it;
+//   3. survivors = items whose approximate entropy is >= T - 2 kApproxErr2,
+//      plus every "special" row (negative / non-finite means, a sum outside
+//      [2^-100, 2^100]: NaN / -inf entropies and the like, which the
+//      approximation does not cover): a superset of the exact top q (q items
+//      are exactly >= T - eps, so an item below T - eps cannot be among them,
+//      and its approximation is below T - 2 eps).  Their rows go to LDS (one
+//      atomic per wave);
+//   4. survivor t evaluates its EXACT entropy (glibc log, scipy's quotients:
+//      bit-identical to the reference), then counts the survivors that beat it
+//      -- (key, ~local slot) triples, a 96-bit subtract's borrow
+//      (add_if_beats) -- and writes itself to output slot `rank` (< q).
+// The exact entropy (the ~150-VALU glibc-log row) runs for the ~q survivors
+// only, not for every item: the keys phase of round 3 was VALU-bound at two
+// blocks per CU (configs[2]).  The local slot v*BS+tid orders a problem's
+// items as their positions do, so no position array stays live.
 // A problem longer than BS*IPT items (a long user of a ragged batch), or more
-// than 64*W survivors (floods of exact ties at the floor), takes per-wave
+// than 64*W survivors (floods of near-ties at the floor), takes per-wave
 // register lists + a tree merge instead (block-uniform branches, same answer).
 #pragma once
 #include "ce_stream.hpp"
@@ -54,40 +64,95 @@ struct TileArgs {
     int64_t base_idx;        // position of item 0 (offsets == nullptr)
 };
 
-template <int WAVES>
+template <int WAVES, int C>
 struct TileSmem {
     static constexpr int CAP = 64 * WAVES;  // one survivor per thread
-    uint4 gb[64];                           // group items (~local slot, key lo, key hi, -)
-    int part[WAVES][64];                    // partial ranks of the group items
+    uint32_t gm[64];                        // group maxima of the approximate keys
+    int part[WAVES][64];                    // partial counts (above | not below << 16)
     int cnt;                                // survivors appended
-    uint4 cs[CAP];                          // survivors (~local slot, key lo, key hi, -)
-    WaveListsT<WAVES> lists;                // fallback tree merge
+    uint4 cs[CAP];                          // survivors' exact (~local slot, key lo, key hi, -)
+    union {
+        struct {
+            double m[C][CAP];               // survivors' exact rows
+            uint32_t nl[CAP];               // ... and ~local slots
+        } sv;
+        WaveListsT<WAVES> lists;            // fallback tree merge
+    };
 };
 
-// Keys of this thread's IPT items lo + tid + BS*v of [lo, hi) into slots
-// [OFF, OFF + IPT): key 0 for a slot past the end or an excluded item (all
-// loads in flight before the arithmetic; COMMIT: `tab` is committed once the
-// data is awaited -- exactly one tile_keys call of a block commits).  Slots
-// outside [OFF, OFF + IPT) are left as they are.
-template <class Src, int IPT, int UNR, int BS, int K, int OFF, bool COMMIT>
-__device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi, const uint32_t* excl,
-                                          LogTablePrefetch& tab, uint64_t (&k)[K]) {
-    static_assert(OFF + IPT <= K, "");
+// Approximate entropy error bound, log2 units, per class: f32 copies of the
+// exact means (2^-24), their f32 sum (C-1 roundings), v_rcp_f32 and v_log_f32
+// (taken as 2^-22 and 2^-21 relative + 2^-20 absolute) give at most ~1.4e-6 *
+// C + 2.1e-6; the bound used is ~8x that, and
+// test_gpu_parity.py::test_approx_entropy_bound measures the device's
+// actual error against it.
+constexpr float kApproxErr2PerClass = 2e-5f;
+
+// The approximate entropy of an exact row as a 32-bit order key (0: never a
+// valid result), and whether the row is special (the exact path decides).
+template <int C>
+__device__ __forceinline__ uint32_t approx_key(const double (&m)[C], bool& special) {
+    float mf[C];
+    uint32_t hw = 0;
+    float S = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t h = (uint32_t)(dbits(m[c]) >> 32);
+        hw = hw > h ? hw : h;  // sign set (negative, -0.0), inf / NaN: >= 0x7ff00000
+        mf[c] = (float)m[c];
+        S += mf[c];
+    }
+    special = hw >= 0x7ff00000u || !(S >= 0x1p-100f && S <= 0x1p100f);
+    const float r = __builtin_amdgcn_rcpf(S);
+    float h = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const float pc = __builtin_fmaxf(mf[c] * r, 0x1p-100f);
+        h = __builtin_fmaf(-pc, __builtin_amdgcn_logf(pc), h);
+    }
+    const uint32_t b = __float_as_uint(h);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+
+__device__ __forceinline__ float approx_key_value(uint32_t k) {
+    return __uint_as_float((k >> 31) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Rows of this thread's IPT items lo + tid + BS*v of [lo, hi) into slots
+// [OFF, OFF + IPT): the exact row in m, its approximate key in ak (0: no item
+// -- past the end, excluded -- or a special row) and sp (special).  COMMIT:
+// `tab` is committed once the first data is awaited -- exactly one tile_rows
+// call of a block commits.  Slots outside [OFF, OFF + IPT) are left as they are.
+template <class Src, int IPT, int UNR, int BS, int K, int C, int OFF, bool COMMIT>
+__device__ __forceinline__ void tile_rows(const Src& src, int64_t lo, int64_t hi, const uint32_t* excl,
+                                          LogTablePrefetch& tab, double (&m)[K][C], uint32_t (&ak)[K],
+                                          bool (&sp)[K]) {
+    static_assert(OFF + IPT <= K && Src::kC == C, "");
     const int tid = threadIdx.x, w = tid >> 6;
     const int64_t len = hi - lo;
     int64_t items[IPT];
-    uint64_t kk[IPT];
     int nlive = 0;  // this wave's item slots holding at least one real item (a prefix)
 #pragma unroll
     for (int v = 0; v < IPT; ++v) {
         const int64_t j = tid + (int64_t)BS * v;
         items[v] = lo + (j < len ? j : (len > 0 ? len - 1 : 0));
-        kk[v] = 0;
         nlive += (int64_t)BS * v + 64 * w < len;
+        ak[OFF + v] = 0;
+        sp[OFF + v] = false;
+#pragma unroll
+        for (int c = 0; c < C; ++c) m[OFF + v][c] = 0.0;
     }
+    auto sink = [&](int u, const double (&row)[C]) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) m[OFF + u][c] = row[c];
+        bool s;
+        const uint32_t a = approx_key<C>(row, s);
+        ak[OFF + u] = s ? 0u : a;
+        sp[OFF + u] = s;
+    };
     if (len > 0) {  // block-uniform
-        if constexpr (COMMIT) src.template keys_small<UNR, IPT>(items, kk, nlive, [&]() { tab.commit(); });
-        else src.template keys_small<UNR, IPT>(items, kk, nlive);
+        if constexpr (COMMIT) src.template rows_small<UNR, IPT>(items, nlive, sink, [&]() { tab.commit(); });
+        else src.template rows_small<UNR, IPT>(items, nlive, sink);
     } else if constexpr (COMMIT) {
         tab.commit();
     }
@@ -95,7 +160,10 @@ __device__ __forceinline__ void tile_keys(const Src& src, int64_t lo, int64_t hi
     for (int v = 0; v < IPT; ++v) {
         bool ok = tid + (int64_t)BS * v < len;
         if (excl) ok = ok && !excluded(excl, items[v]);
-        k[OFF + v] = ok ? kk[v] : 0ull;
+        if (!ok) {
+            ak[OFF + v] = 0;
+            sp[OFF + v] = false;
+        }
     }
 }
 
@@ -115,23 +183,18 @@ __device__ __forceinline__ int add_if_beats(int r, const uint4& m, const uint4& 
     return out;
 }
 
-// The max key of each group of GS lanes (and the slot of one item holding it)
-// in the group's lanes: DPP mirrors within quads, half rows and rows.
+// The max of each group of GS lanes in the group's lanes: DPP mirrors within
+// quads, half rows and rows (one v_max per step).
 template <int GS>
-__device__ __forceinline__ void group_max(uint64_t& k, uint32_t& n) {
-#define CE_GM(J, CTL)                                                                                  \
-    if constexpr (GS > J) {                                                                            \
-        const uint32_t p0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)k, CTL, 0xF, 0xF, false);         \
-        const uint32_t p1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(k >> 32), CTL, 0xF, 0xF, false); \
-        const uint32_t pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n, CTL, 0xF, 0xF, false);                   \
-        const uint64_t pk = ((uint64_t)p1 << 32) | p0;                                                 \
-        if (pk > k) {                                                                                  \
-            k = pk;                                                                                    \
-            n = pn;                                                                                    \
-        }                                                                                              \
+__device__ __forceinline__ uint32_t group_max(uint32_t k) {
+#define CE_GM(J, CTL)                                                                              \
+    if constexpr (GS > J) {                                                                        \
+        const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, CTL, 0xF, 0xF, false); \
+        k = k > o ? k : o;                                                                         \
     }
     CE_GM(1, 0xB1) CE_GM(2, 0x4E) CE_GM(4, 0x141) CE_GM(8, 0x140)  // quad [1,0,3,2], [2,3,0,1]; half-row, row mirror
 #undef CE_GM
+    return k;
 }
 
 // LONG: a problem may exceed BS * IPT items (the per-wave streaming path is
@@ -144,7 +207,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
     constexpr int K = IPTA + IPTB;  // slots: segment A's, then segment B's (both segments in one block)
     static_assert(BS % 64 == 0 && BS >= 128 && GS <= 16 && (GS & (GS - 1)) == 0, "block size");
-    using SM = TileSmem<W>;
+    constexpr int C = SrcA::kC;
+    static_assert(IPTB == 0 || SrcB::kC == C, "both segments' rows have C classes");
+    using SM = TileSmem<W, C>;
     __shared__ SM sm;
     CE_STAMP(blockIdx.x, 0)
     LogTablePrefetch tab;
@@ -185,78 +250,68 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
         return;
     } else {
-        // 1. keys of this thread's items
-        uint64_t kz[K];  // key 0: no item
-#pragma unroll
-        for (int v = 0; v < K; ++v) kz[v] = 0;
-        tile_keys<SrcA, IPTA, UNRA, BS, K, 0, true>(srcA, lo, hi, excl, tab, kz);
+        // 1. exact rows + approximate keys of this thread's items
+        double mrow[K][C];
+        uint32_t ak[K];
+        bool sp[K];
+        tile_rows<SrcA, IPTA, UNRA, BS, K, C, 0, true>(srcA, lo, hi, excl, tab, mrow, ak, sp);
         if constexpr (IPTB > 0)
-            if (both) tile_keys<SrcB, IPTB, UNRB, BS, K, IPTA, false>(srcB, 0, ta.nB, nullptr, tab, kz);
+            if (both) tile_rows<SrcB, IPTB, UNRB, BS, K, C, IPTA, false>(srcB, 0, ta.nB, nullptr, tab, mrow, ak, sp);
         CE_STAMP(blockIdx.x, 1)
         CE_WSTAMP(blockIdx.x)
-        // 2. every slot as a triple (~local slot, key lo, key hi): local slot
-        //    L = v * BS + tid orders the block's items as their positions do,
-        //    so "a beats b" is the 96-bit compare of the triples (key 0: no item)
         const uint32_t ntid = ~(uint32_t)tid;
-        uint32_t nl[K];
-#pragma unroll
-        for (int v = 0; v < K; ++v) nl[v] = ntid - (uint32_t)(v * BS);  // ~(v * BS + tid)
-        // the lane's max key, its lowest slot on ties; then the group's max key
-        // (a tie keeps the lane's own item: any item holding the group's max
-        // key stands for the group -- 64 distinct items)
-        uint64_t bk = kz[0];
-        uint32_t bn = nl[0];
-#pragma unroll
-        for (int v = 1; v < K; ++v)
-            if (kz[v] > bk) {
-                bk = kz[v];
-                bn = nl[v];
-            }
-        group_max<GS>(bk, bn);
-        if ((tid & (GS - 1)) == 0) sm.gb[tid / GS] = make_uint4(bn, (uint32_t)bk, (uint32_t)(bk >> 32), 0u);
-        if (tid == 0) sm.cnt = 0;
-        __syncthreads();
-        // floor = the group item of rank q-1 (ranks split over the waves; the
-        // 64 triples are distinct, so exactly one lane holds rank q-1 <= 63)
-        const uint4 mg = sm.gb[lane];
-        {
-            int r = 0;
-#pragma unroll
-            for (int j = 0; j < 64 / W; ++j) r = add_if_beats(r, mg, sm.gb[w * (64 / W) + j]);
-            sm.part[w][lane] = r;
-        }
-        __syncthreads();
-        uint64_t fk;
-        uint32_t fn;
-        {
-            int r = 0;
-#pragma unroll
-            for (int j = 0; j < W; ++j) r += sm.part[j][lane];
-            const int sl = __builtin_ctzll(__ballot(r == q - 1));
-            fn = (uint32_t)__builtin_amdgcn_readlane((int)mg.x, sl);
-            fk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mg.z, sl) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)mg.y, sl);
-        }
-        const bool floor = fk != 0;  // else fewer than q groups hold an item: admit every item
-        if (!floor) fn = 0;
-        if (!floor) fk = 1;  // every valid key is > 1, key 0 (no item) is not
         // position of local slot L (segment A's slots first, then segment B's)
         auto pos_of = [&](uint32_t L) -> int64_t {
             return L < (uint32_t)(IPTA * BS) ? lo + rel + (int64_t)L : (int64_t)(L - (uint32_t)(IPTA * BS)) + relB;
         };
+        // 2. T = the group maximum of rank q-1 (with multiplicity): q distinct
+        //    items have approximate keys >= T
+        uint32_t bk = ak[0];
+#pragma unroll
+        for (int v = 1; v < K; ++v) bk = bk > ak[v] ? bk : ak[v];
+        bk = group_max<GS>(bk);
+        if ((tid & (GS - 1)) == 0) sm.gm[tid / GS] = bk;
+        if (tid == 0) sm.cnt = 0;
+        __syncthreads();
+        const uint32_t mg = sm.gm[lane];
+        {
+            int r = 0;
+#pragma unroll
+            for (int j = 0; j < 64 / W; ++j) {
+                const uint32_t o = sm.gm[w * (64 / W) + j];
+                r += (o > mg ? 1 : 0) + (o >= mg ? 0x10000 : 0);
+            }
+            sm.part[w][lane] = r;
+        }
+        __syncthreads();
+        uint32_t thr;  // survivors: approximate key >= thr (>= 1: never a slot without an item)
+        {
+            int r = 0;
+#pragma unroll
+            for (int j = 0; j < W; ++j) r += sm.part[j][lane];
+            const int above = r & 0xffff, notbelow = r >> 16;
+            const int sl = __builtin_ctzll(__ballot(above < q && notbelow >= q));
+            const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)mg, sl);
+            thr = 1;
+            if (T != 0) {  // else fewer than q ordinary items: every item survives
+                const float lim = approx_key_value(T) - 2.0f * kApproxErr2PerClass * C;
+                const uint32_t b = __float_as_uint(lim);
+                const uint32_t tk = (b >> 31) ? ~b : (b | 0x80000000u);
+                thr = tk > 1 ? tk : 1;
+            }
+        }
         CE_STAMP(blockIdx.x, 2)
-        // 3. survivors (not worse than the floor) -> LDS list: the wave's K
-        //    ballots first, then ONE atomic per wave for all of its survivors
-        //    (each returning LDS atomic is a ~100-cycle round trip)
+        // 3. survivors -> LDS rows: the wave's K ballots first, then ONE atomic
+        //    per wave for all of its survivors
         {
             bool pass[K];
-            uint64_t m[K];
+            uint64_t msk[K];
             int tot = 0;
 #pragma unroll
             for (int v = 0; v < K; ++v) {
-                pass[v] = (kz[v] > fk) | ((kz[v] == fk) & (nl[v] >= fn));  // bitwise: no per-slot branches
-                m[v] = __ballot(pass[v]);
-                tot += __popcll(m[v]);
+                pass[v] = sp[v] | (ak[v] >= thr);
+                msk[v] = __ballot(pass[v]);
+                tot += __popcll(msk[v]);
             }
             if (tot) {  // wave-uniform
                 int base = 0;
@@ -264,11 +319,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 base = __builtin_amdgcn_readfirstlane(base);
 #pragma unroll
                 for (int v = 0; v < K; ++v) {
-                    const int slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[v] >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m[v], 0));
-                    if (pass[v] && slot < SM::CAP)
-                        sm.cs[slot] = make_uint4(nl[v], (uint32_t)kz[v], (uint32_t)(kz[v] >> 32), 0u);
-                    base += __popcll(m[v]);
+                    const int slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(msk[v] >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)msk[v], 0));
+                    if (pass[v] && slot < SM::CAP) {
+#pragma unroll
+                        for (int c = 0; c < C; ++c) sm.sv.m[c][slot] = mrow[v][c];
+                        sm.sv.nl[slot] = ntid - (uint32_t)(v * BS);  // ~(v * BS + tid)
+                    }
+                    base += __popcll(msk[v]);
                 }
             }
         }
@@ -276,6 +334,15 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         CE_STAMP(blockIdx.x, 3)
         const int nc = sm.cnt;
         if (nc <= SM::CAP) {
+            // 4. exact entropies of the survivors, then ranks
+            if (tid < nc) {
+                double row[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) row[c] = sm.sv.m[c][tid];
+                const uint64_t key = order_key(entropy_row<C>(row));
+                sm.cs[tid] = make_uint4(sm.sv.nl[tid], (uint32_t)key, (uint32_t)(key >> 32), 0u);
+            }
+            __syncthreads();
             if (tid < nc) {  // survivor tid takes the slot of its rank
                 const uint4 me = sm.cs[tid];
                 int r = 0;
@@ -291,12 +358,16 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
             }
             CE_STAMP(blockIdx.x, 4)
         } else {
-            // overflow (> CAP items tie at or above the floor): per-wave lists + tree merge
+            // overflow (> CAP items at or near the floor): exact keys of every
+            // item, per-wave lists + tree merge
             RegTopQ tq;
-            if (floor) tq.init(q, fk, pos_of(~fn) + 1);  // admit candidates >= the floor
-            else tq.init(q, 0, INT64_MAX);
+            tq.init(q);
 #pragma unroll
-            for (int v = 0; v < K; ++v) tq.offer(kz[v], pos_of(~nl[v]), kz[v] != 0);
+            for (int v = 0; v < K; ++v) {
+                const bool ok = sp[v] | (ak[v] != 0);
+                const uint64_t key = ok ? order_key(entropy_row<C>(mrow[v])) : 0ull;
+                tq.offer(key, pos_of((uint32_t)(v * BS + tid)), ok);
+            }
             block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
         }
     }
