@@ -43,6 +43,7 @@ SIGNATURES = {
     "ce_log_f64_host": (_int, [_vp, _i64, _vp]),
     "ce_exp_f64": (_int, [_vp, _i64, _vp, _vp]),
     "ce_exp_f64_host": (_int, [_vp, _i64, _vp]),
+    "ce_approx_entropy": (_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
     "ce_row_div_f64": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "ce_segment_mean": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _vp, _i64, _vp, _int, _i64, _vp]),
     "ce_select_frames_workspace_bytes": (_sz, [_i64, _i32]),

@@ -128,6 +128,21 @@ def exp_f64(x):
     return y
 
 
+def approx_entropy(rows):
+    """The single-block pools' approximate entropy of exact consensus rows
+    [n, C] f64 (ce_approx_entropy: log2 units, f32) and their special flags
+    (verification of the prefilter's error bound)."""
+    _on_gpu(rows, "rows")
+    rows = rows.contiguous()
+    if rows.dtype != torch.float64 or rows.dim() != 2:
+        raise ValueError("approx_entropy takes [n, C] float64")
+    n, C = rows.shape
+    h2 = torch.empty(n, dtype=torch.float32, device=rows.device)
+    sp = torch.empty(n, dtype=torch.uint8, device=rows.device)
+    call("ce_approx_entropy", _p(rows), n, C, _p(h2), _p(sp), _stream(rows.device))
+    return h2, sp.bool()
+
+
 def row_div_f64(x, s):
     """x / s as the engine divides each consensus row by its sum inside the
     entropy (ce_row_div_f64: one reciprocal per row; verification against

@@ -122,6 +122,38 @@ extern "C" int ce_exp_f64(const double* x, int64_t n, double* y, ce_stream_t str
     return check_launch("ce_exp_f64");
 }
 
+// the small pools' approximate entropy (ce_device.hpp approx_key) of n exact
+// rows [n, C]: log2 units, and the special flag (those rows take the exact path)
+template <int C>
+__global__ __launch_bounds__(kBS) void k_approx(const double* __restrict__ rows, int64_t n, float* __restrict__ h2,
+                                                uint8_t* __restrict__ special) {
+    for (int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBS) {
+        double m[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) m[c] = rows[i * C + c];
+        bool sp;
+        const uint32_t k = approx_key<C>(m, sp);
+        h2[i] = approx_key_value(k);
+        special[i] = sp ? 1 : 0;
+    }
+}
+
+extern "C" int ce_approx_entropy(const double* rows, int64_t n, int32_t C, float* h2, uint8_t* special,
+                                 ce_stream_t stream) {
+    if (n < 0 || (n > 0 && (!rows || !h2 || !special))) return fail(CE_EINVAL, "bad approx-entropy arguments");
+    if (n == 0) return CE_OK;
+    const int grid = (int)std::min<int64_t>(cdiv(n, kBS), 8192);
+    const hipStream_t st = (hipStream_t)stream;
+    switch (C) {
+        case 2: hipLaunchKernelGGL(k_approx<2>, dim3(grid), dim3(kBS), 0, st, rows, n, h2, special); break;
+        case 3: hipLaunchKernelGGL(k_approx<3>, dim3(grid), dim3(kBS), 0, st, rows, n, h2, special); break;
+        case 4: hipLaunchKernelGGL(k_approx<4>, dim3(grid), dim3(kBS), 0, st, rows, n, h2, special); break;
+        case 8: hipLaunchKernelGGL(k_approx<8>, dim3(grid), dim3(kBS), 0, st, rows, n, h2, special); break;
+        default: return fail(CE_EINVAL, "approx entropy: C must be 2, 3, 4 or 8 (the single-block pools' classes)");
+    }
+    return check_launch("ce_approx_entropy");
+}
+
 extern "C" int ce_exp_f64_host(const double* x, int64_t n, double* y) {
     if (n < 0 || (n > 0 && (!x || !y))) return fail(CE_EINVAL, "bad exp arguments");
     const uint64_t* tab = host_exp_table();

@@ -135,6 +135,28 @@ __device__ __forceinline__ void row_quotients(const double (&x)[C], double s, do
     for (int c = 0; c < C; ++c) d[c] = x[c] / s;
 }
 
+// One of row_quotients' quotients, xc = x[c]: the same range test over the
+// whole row, the same operations on xc -- bit-identical to d[c].
+template <int C>
+__device__ __forceinline__ double row_quotient_one(const double (&x)[C], double s, double xc) {
+    const uint32_t hs = (uint32_t)(dbits(s) >> 32);
+    uint32_t lo = hs, hi = hs;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t h = (uint32_t)(dbits(x[c]) >> 32);
+        lo = lo < h ? lo : h;
+        hi = hi > h ? hi : h;
+    }
+    if (__builtin_expect(lo >= (723u << 20) && hi < (1323u << 20), 1)) {
+        double r = __builtin_amdgcn_rcp(s);
+        r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
+        r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
+        const double q = xc * r;
+        return __builtin_fma(__builtin_fma(-s, q, xc), r, q);
+    }
+    return xc / s;
+}
+
 // scipy.stats.entropy of one row held in registers (mean: consensus row).
 template <int C>
 __device__ __forceinline__ double entropy_row(const double (&mean)[C]) {
@@ -150,6 +172,44 @@ __device__ __forceinline__ double entropy_row(const double (&mean)[C]) {
 #pragma unroll
     for (int c = 0; c < C; ++c) e[c] = entr(1.0 * mean[c] / s);
     return row_sum<C>(e);
+}
+
+// Approximate entropy error bound, log2 units, per class: f32 copies of the
+// exact means (2^-24), their f32 sum (C-1 roundings), v_rcp_f32 and v_log_f32
+// (taken as 2^-22 and 2^-21 relative + 2^-20 absolute) give at most ~1.4e-6 *
+// C + 2.1e-6; the bound used is ~8x that, and
+// tests/test_gpu_parity.py::test_approx_entropy_bound (via ce_approx_entropy) measures the device's
+// actual error against it.
+constexpr float kApproxErr2PerClass = 2e-5f;
+
+// The approximate entropy of an exact row as a 32-bit order key (0: never a
+// valid result), and whether the row is special (the exact path decides).
+template <int C>
+__device__ __forceinline__ uint32_t approx_key(const double (&m)[C], bool& special) {
+    float mf[C];
+    uint32_t hw = 0;
+    float S = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t h = (uint32_t)(dbits(m[c]) >> 32);
+        hw = hw > h ? hw : h;  // sign set (negative, -0.0), inf / NaN: >= 0x7ff00000
+        mf[c] = (float)m[c];
+        S += mf[c];
+    }
+    special = hw >= 0x7ff00000u || !(S >= 0x1p-100f && S <= 0x1p100f);
+    const float r = __builtin_amdgcn_rcpf(S);
+    float h = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const float pc = __builtin_fmaxf(mf[c] * r, 0x1p-100f);
+        h = __builtin_fmaf(-pc, __builtin_amdgcn_logf(pc), h);
+    }
+    const uint32_t b = __float_as_uint(h);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+
+__device__ __forceinline__ float approx_key_value(uint32_t k) {
+    return __uint_as_float((k >> 31) ? (k & 0x7fffffffu) : ~k);
 }
 
 // mean = acc / M as numpy's true_divide; a power-of-two M divides exactly by a

@@ -48,6 +48,9 @@ constexpr int kSegWaves = 16;     // waves per single-block pool / per user (k_s
 // item slots a lane keeps in flight in the single-block pools (rows_small).
 // Measured on configs[2] (500 users x 1608, f32): all at once 14.24 us,
 // 1 slot 13.52 us, 2 slots 14.68 us
+// Round 4, after the approximate prefilter (profiles/r04_small_phase_prefilter.json):
+// 1 slot 10.74 us, 2 slots 10.98 us, all 16-23 us (register spills);
+// the last short slot issued with slot 0: C1 6.12 -> 6.42 us, C3 even.
 constexpr int kSmallThrottle = 1;
 
 template <int DT, int C, bool VEC>
@@ -124,24 +127,23 @@ struct CommitteeSrc {
         // THR item slots in flight per lane (THR < IPL: slot u + THR is issued
         // only once slot u has landed, so every block keeps a bounded share of
         // the memory queues instead of all of its bytes at once)
-        // (the last, short slot of a pool -- 72 of 1608 items -- issued with slot 0
-        // measured slower: C1 7.56 -> 8.56 us, C3 12.64 -> 13.08 us, r04_small_ab.json)
         constexpr int D = (THR > 0 && THR < IPL) ? THR : IPL;
 #pragma unroll
-        for (int u = 0; u < D; ++u) issue(u);
+        for (int i = 0; i < D; ++i) issue(i);
         hook();
         auto item = [&](auto full) {
 #pragma unroll
-            for (int u = 0; u < IPL; ++u) {
+            for (int i = 0; i < IPL; ++i) {
+                const int u = i;
                 if constexpr (D < IPL) {
-                    if (u + D < IPL) {
+                    if (i + D < IPL) {
                         // slot u landed (the asm reads its registers: the compiler waits
-                        // for exactly those loads), then slot u + D is issued; the
+                        // for exactly those loads), then the next slot is issued; the
                         // memory clobber keeps that issue behind the wait
 #pragma unroll
                         for (int v = 0; v < UNR; ++v) ld[u][v].pin();
                         asm volatile("" ::: "memory");
-                        issue(u + D);
+                        issue(i + D);
                     }
                 }
                 if (u >= nlive) continue;  // wave-uniform

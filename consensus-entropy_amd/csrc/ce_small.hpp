@@ -20,10 +20,15 @@
 //      are exactly >= T - eps, so an item below T - eps cannot be among them,
 //      and its approximation is below T - 2 eps).  Their rows go to LDS (one
 //      atomic per wave);
-//   4. survivor t evaluates its EXACT entropy (glibc log, scipy's quotients:
-//      bit-identical to the reference), then counts the survivors that beat it
-//      -- (key, ~local slot) triples, a 96-bit subtract's borrow
-//      (add_if_beats) -- and writes itself to output slot `rank` (< q).
+//   4. the survivors' EXACT entropies (glibc log, scipy's quotients:
+//      bit-identical to the reference), P = C rounded up to 2/4/8 lanes per
+//      survivor, one class per lane (the wave issues each instruction once
+//      for all lanes: one log chain instead of C in a row), terms gathered by
+//      lane shuffles and summed in numpy's order; then every survivor counts
+//      the survivors that beat it -- (key, ~local slot) triples, a 96-bit
+//      subtract's borrow (add_if_beats) -- and writes itself to output slot
+//      `rank` (< q).  Up to 64/P survivors (the usual case) are evaluated and
+//      ranked by wave 0 alone, with no second block barrier.
 // The exact entropy (the ~150-VALU glibc-log row) runs for the ~q survivors
 // only, not for every item: the keys phase of round 3 was VALU-bound at two
 // blocks per CU (configs[2]).  The local slot v*BS+tid orders a problem's
@@ -79,44 +84,6 @@ struct TileSmem {
         WaveListsT<WAVES> lists;            // fallback tree merge
     };
 };
-
-// Approximate entropy error bound, log2 units, per class: f32 copies of the
-// exact means (2^-24), their f32 sum (C-1 roundings), v_rcp_f32 and v_log_f32
-// (taken as 2^-22 and 2^-21 relative + 2^-20 absolute) give at most ~1.4e-6 *
-// C + 2.1e-6; the bound used is ~8x that, and
-// test_gpu_parity.py::test_approx_entropy_bound measures the device's
-// actual error against it.
-constexpr float kApproxErr2PerClass = 2e-5f;
-
-// The approximate entropy of an exact row as a 32-bit order key (0: never a
-// valid result), and whether the row is special (the exact path decides).
-template <int C>
-__device__ __forceinline__ uint32_t approx_key(const double (&m)[C], bool& special) {
-    float mf[C];
-    uint32_t hw = 0;
-    float S = 0.0f;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        const uint32_t h = (uint32_t)(dbits(m[c]) >> 32);
-        hw = hw > h ? hw : h;  // sign set (negative, -0.0), inf / NaN: >= 0x7ff00000
-        mf[c] = (float)m[c];
-        S += mf[c];
-    }
-    special = hw >= 0x7ff00000u || !(S >= 0x1p-100f && S <= 0x1p100f);
-    const float r = __builtin_amdgcn_rcpf(S);
-    float h = 0.0f;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        const float pc = __builtin_fmaxf(mf[c] * r, 0x1p-100f);
-        h = __builtin_fmaf(-pc, __builtin_amdgcn_logf(pc), h);
-    }
-    const uint32_t b = __float_as_uint(h);
-    return (b >> 31) ? ~b : (b | 0x80000000u);
-}
-
-__device__ __forceinline__ float approx_key_value(uint32_t k) {
-    return __uint_as_float((k >> 31) ? (k & 0x7fffffffu) : ~k);
-}
 
 // Rows of this thread's IPT items lo + tid + BS*v of [lo, hi) into slots
 // [OFF, OFF + IPT): the exact row in m, its approximate key in ak (0: no item
@@ -201,7 +168,7 @@ __device__ __forceinline__ uint32_t group_max(uint32_t k) {
 // compiled in).  Launches whose host checks bound the problem (one pool, the
 // mix) drop it -- half the code of the kernel.
 template <class SrcA, class SrcB, int IPTA, int IPTB, int UNRA, int UNRB, int BS, bool LONG = true>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_select_tiles(
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : BS / 256))) void k_select_tiles(
     SrcA srcA, SrcB srcB, TileArgs ta, int q, double* __restrict__ oval, int64_t* __restrict__ oidx,
     const uint32_t* __restrict__ excl) {
     constexpr int W = BS / 64, GS = BS / 64;  // waves; lanes per group (64 groups)
@@ -334,17 +301,33 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         CE_STAMP(blockIdx.x, 3)
         const int nc = sm.cnt;
         if (nc <= SM::CAP) {
-            // 4. exact entropies of the survivors, then ranks
-            if (tid < nc) {
-                double row[C];
+            // 4. exact entropies of the survivors, P lanes per survivor (one
+            //    class each: one glibc log per lane instead of C in a row --
+            //    the wave issues each instruction once for all its lanes), the
+            //    terms gathered by lane shuffles and summed in numpy's order;
+            //    then ranks.  Up to 64/P survivors (the usual case) stay in
+            //    wave 0: no second block barrier.
+            constexpr int P = C <= 2 ? 2 : (C <= 4 ? 4 : 8);
+            constexpr int SPW = 64 / P;
+            static_assert(C <= 8, "single-block pools hold rows of <= 8 classes");
+#pragma unroll 1
+            for (int t0 = w * SPW; t0 < nc; t0 += W * SPW) {  // wave-uniform
+                const int t = t0 + lane / P, c = lane % P;
+                const int ts = t < nc ? t : 0;
+                double x[C];
 #pragma unroll
-                for (int c = 0; c < C; ++c) row[c] = sm.sv.m[c][tid];
-                const uint64_t key = order_key(entropy_row<C>(row));
-                sm.cs[tid] = make_uint4(sm.sv.nl[tid], (uint32_t)key, (uint32_t)(key >> 32), 0u);
+                for (int cc = 0; cc < C; ++cc) x[cc] = sm.sv.m[cc][ts];
+                const double xc = sm.sv.m[c < C ? c : 0][ts];
+                const double s = row_sum<C>(x);
+                const double e = entr(row_quotient_one<C>(x, s, xc));
+                double ee[C];
+#pragma unroll
+                for (int j = 0; j < C; ++j) ee[j] = __shfl(e, (lane & ~(P - 1)) + j);
+                const uint64_t key = order_key(row_sum<C>(ee));
+                if (t < nc && c == 0) sm.cs[t] = make_uint4(sm.sv.nl[t], (uint32_t)key, (uint32_t)(key >> 32), 0u);
             }
-            __syncthreads();
-            if (tid < nc) {  // survivor tid takes the slot of its rank
-                const uint4 me = sm.cs[tid];
+            auto rank_write = [&](int i) {  // survivor i takes the slot of its rank
+                const uint4 me = sm.cs[i];
                 int r = 0;
 #pragma unroll 8
                 for (int j = 0; j < nc; ++j) r = add_if_beats(r, me, sm.cs[j]);
@@ -352,9 +335,22 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                     ov[r] = key_to_val(((uint64_t)me.z << 32) | me.y);
                     oi[r] = pos_of(~me.x);
                 }
-            } else if (tid < q) {  // fewer survivors than q: padding
-                ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
-                oi[tid] = -1;
+            };
+            auto pad = [&](int i) {  // fewer survivors than q: padding
+                ov[i] = __longlong_as_double(0x7ff8000000000000ll);
+                oi[i] = -1;
+            };
+            if (nc <= SPW) {  // block-uniform: wave 0 wrote every triple and ranks them
+                if (w == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane < nc) rank_write(lane);
+                    else if (lane < q) pad(lane);
+                }
+            } else {
+                __syncthreads();
+                if (tid < nc) rank_write(tid);
+                else if (tid < q) pad(tid);
             }
             CE_STAMP(blockIdx.x, 4)
         } else {

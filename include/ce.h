@@ -210,6 +210,11 @@ int ce_log_f64_host(const double *x, int64_t n, double *y);
  * (synchronous, no GPU) builds, for verification against the C library. */
 int ce_exp_f64(const double *x, int64_t n, double *y, ce_stream_t stream);
 int ce_exp_f64_host(const double *x, int64_t n, double *y);
+/* The single-block pools' approximate entropy (f32, hardware rcp / log2; the
+ * prefilter of csrc/ce_small.hpp) of n exact consensus rows [n, C] (C in
+ * {2, 3, 4, 8}), in log2 units, and whether each row is special (taken by the
+ * exact path): verification of the error bound the prefilter's floor relies on. */
+int ce_approx_entropy(const double *rows, int64_t n, int32_t C, float *h2, uint8_t *special, ce_stream_t stream);
 
 /*
  * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]

@@ -279,6 +279,60 @@ def test_device_exp_bit_exact(ce):
     assert bad == 0
 
 
+def test_approx_entropy_bound(ce):
+    """The single-block pools' prefilter (csrc/ce_small.hpp) admits every item
+    whose approximate entropy is within 2 * kApproxErr2PerClass * C (log2
+    units) of the floor; that is a superset of the exact top q only if the
+    device's f32 approximation (hardware rcp / log2) stays within
+    kApproxErr2PerClass * C of the exact entropy.  Measured here on 1.3e7 rows
+    -- Dirichlet rows from very peaked to near-uniform, zeros, classes down to
+    1e-300, unnormalised rows with sums across [2^-100, 2^100] -- against the
+    exact restatement, with a 4x margin; the special flag (rows the exact path
+    takes: negative / -0.0 / non-finite means, f32 sums outside [2^-100,
+    2^100]) must match its rule exactly."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(4242)
+    worst = {}
+    for C in (2, 3, 4, 8):
+        parts = []
+        for a in (0.02, 0.2, 1.0, 5.0, 100.0):
+            parts.append(rng.dirichlet(np.full(C, a), 400_000))
+        z = rng.dirichlet(np.ones(C), 300_000)
+        z[rng.random(z.shape) < 0.3] = 0.0  # zero classes (and some all-zero rows: special)
+        parts.append(z)
+        t = rng.dirichlet(np.ones(C), 300_000)
+        t[:, 0] = 10.0 ** rng.uniform(-300, -20, len(t))  # tiny classes, f64 and f32-denormal range
+        parts.append(t)
+        u = rng.dirichlet(np.ones(C), 300_000) * (10.0 ** rng.uniform(-30.5, 30.5, (300_000, 1)))
+        parts.append(u)  # unnormalised, sums across (and a little beyond) [2^-100, 2^100]
+        v = np.full((200_000, C), 1.0 / C) + rng.normal(0, 1e-7, (200_000, C))
+        parts.append(np.abs(v))  # near-uniform
+        sp = rng.dirichlet(np.ones(C), 20_000)
+        k = rng.integers(0, 5, len(sp))
+        sp[k == 0, 0] = -sp[k == 0, 0]
+        sp[k == 1, 0] = np.nan
+        sp[k == 2, 0] = np.inf
+        sp[k == 3, 0] = -0.0
+        parts.append(sp)
+        R = np.ascontiguousarray(np.concatenate(parts))
+        h2, spec = ce.ops.approx_entropy(dev(R))
+        h2, spec = h2.cpu().numpy().astype(np.float64), spec.cpu().numpy()
+        mf = R.astype(np.float32)
+        S = np.zeros(len(R), np.float32)
+        for c in range(C):
+            S = (S + mf[:, c]).astype(np.float32)
+        rule = (np.signbit(R) | ~np.isfinite(R)).any(1) | ~((S >= np.float32(2.0 ** -100)) & (S <= np.float32(2.0 ** 100)))
+        assert np.array_equal(spec, rule), C
+        ok = ~spec
+        exact = O.oracle_table_entropy(R[ok]) / np.log(2.0)
+        err = np.abs(h2[ok] - exact)
+        bound = 2e-5 * C  # kApproxErr2PerClass * C
+        worst[C] = float(err.max())
+        assert err.max() <= bound / 4, (C, float(err.max()), bound)
+    print("max |approx - exact| (log2 units) per C:", worst)
+
+
 def test_row_division_bit_exact(ce):
     """The entropy's row division (one shared reciprocal per row, exact by
     construction -- DESIGN.md 'Numerics') equals IEEE x / s on 6e7 pairs:
