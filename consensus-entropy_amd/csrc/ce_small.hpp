@@ -43,7 +43,7 @@ namespace ce {
 
 #ifdef CE_PHASE_TIMING
 // diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
-// [0] start, [1] wave 0's keys done, [2] floor, [3] append, [4] rank, [5] merge,
+// [0] start, [1] wave 0's keys done, [2] floor, [3] append, [4] rank, [5] exact keys (wave 0),
 // [6 + w] wave w's keys done (w < 8)
 __device__ uint64_t g_phase[8192][16];
 // [14], [15]: shader-clock counter at [0] and [4] (the clock rate over the block)
@@ -75,7 +75,7 @@ struct TileSmem {
     uint32_t gm[64];                        // group maxima of the approximate keys
     int part[WAVES][64];                    // partial counts (above | not below << 16)
     int cnt;                                // survivors appended
-    uint4 cs[CAP];                          // survivors' exact (~local slot, key lo, key hi, -)
+    uint4 cs[CAP + 8];                      // survivors' exact (~local slot, key lo, key hi, -), + 8 zero triples
     union {
         struct {
             double m[C][CAP];               // survivors' exact rows
@@ -310,6 +310,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
             constexpr int P = C <= 2 ? 2 : (C <= 4 ? 4 : 8);
             constexpr int SPW = 64 / P;
             static_assert(C <= 8, "single-block pools hold rows of <= 8 classes");
+            if (tid < 8) sm.cs[nc + tid] = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll 1
             for (int t0 = w * SPW; t0 < nc; t0 += W * SPW) {  // wave-uniform
                 const int t = t0 + lane / P, c = lane % P;
@@ -326,11 +327,22 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
                 const uint64_t key = order_key(row_sum<C>(ee));
                 if (t < nc && c == 0) sm.cs[t] = make_uint4(sm.sv.nl[t], (uint32_t)key, (uint32_t)(key >> 32), 0u);
             }
+            CE_STAMP(blockIdx.x, 5)
             auto rank_write = [&](int i) {  // survivor i takes the slot of its rank
                 const uint4 me = sm.cs[i];
                 int r = 0;
-#pragma unroll 8
-                for (int j = 0; j < nc; ++j) r = add_if_beats(r, me, sm.cs[j]);
+                // 8 triples per LDS round trip (the asm keeps the compiler from
+                // unrolling a runtime-bounded loop itself: one round trip per
+                // survivor measured 0.84 us); cs[nc, nc + 8) holds zero triples,
+                // which beat nothing
+#pragma unroll 1
+                for (int j0 = 0; j0 < nc; j0 += 8) {
+                    uint4 a[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) a[k] = sm.cs[j0 + k];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) r = add_if_beats(r, me, a[k]);
+                }
                 if (r < q) {
                     ov[r] = key_to_val(((uint64_t)me.z << 32) | me.y);
                     oi[r] = pos_of(~me.x);

@@ -39,7 +39,8 @@ def reduce(b):
             "keys_ns": pct(t[:, 1] - t[:, 0]),
             "floor_ns": pct(t[:, 2] - t[:, 1]),
             "append_ns": pct(t[:, 3] - t[:, 2]),
-            "rank_ns": pct(t[:, 4] - t[:, 3]),
+            "exact_ns": pct(t[:, 5] - t[:, 3]),  # survivors' exact entropies (wave 0's share)
+            "rank_ns": pct(t[:, 4] - t[:, 5]),
             "end_ns": pct(t[:, 4]),
             # per-wave key ends (waves 0..7): the block's slowest / fastest wave, and the intra-block skew
             "wave_keys_last_ns": pct(t[:, 6:14].max(1) - t[:, 0]),
