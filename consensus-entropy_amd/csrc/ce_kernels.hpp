@@ -45,13 +45,6 @@ constexpr int kSegWaves = 16;     // waves per single-block pool / per user (k_s
 // ---------------------------------------------------------------------------
 
 
-// item slots a lane keeps in flight in the single-block pools (rows_small).
-// Measured on configs[2] (500 users x 1608, f32): all at once 14.24 us,
-// 1 slot 13.52 us, 2 slots 14.68 us
-// Round 4, after the approximate prefilter (profiles/r04_small_phase_prefilter.json):
-// 1 slot 10.74 us, 2 slots 10.98 us, all 16-23 us (register spills);
-// the last short slot issued with slot 0: C1 6.12 -> 6.42 us, C3 even.
-constexpr int kSmallThrottle = 1;
 
 template <int DT, int C, bool VEC>
 struct CommitteeSrc {

@@ -90,7 +90,7 @@ struct TileSmem {
 // -- past the end, excluded -- or a special row) and sp (special).  COMMIT:
 // `tab` is committed once the first data is awaited -- exactly one tile_rows
 // call of a block commits.  Slots outside [OFF, OFF + IPT) are left as they are.
-template <class Src, int IPT, int UNR, int BS, int K, int C, int OFF, bool COMMIT>
+template <class Src, int IPT, int UNR, int BS, int K, int C, int OFF, bool COMMIT, int THR = kSmallThrottle>
 __device__ __forceinline__ void tile_rows(const Src& src, int64_t lo, int64_t hi, const uint32_t* excl,
                                           LogTablePrefetch& tab, double (&m)[K][C], uint32_t (&ak)[K],
                                           bool (&sp)[K]) {
@@ -118,8 +118,9 @@ __device__ __forceinline__ void tile_rows(const Src& src, int64_t lo, int64_t hi
         sp[OFF + u] = s;
     };
     if (len > 0) {  // block-uniform
-        if constexpr (COMMIT) src.template rows_small<UNR, IPT>(items, nlive, sink, [&]() { tab.commit(); });
-        else src.template rows_small<UNR, IPT>(items, nlive, sink);
+        auto commit = [&]() { tab.commit(); };
+        if constexpr (COMMIT) src.template rows_small<UNR, IPT, decltype(sink)&, decltype(commit), THR>(items, nlive, sink, commit);
+        else src.template rows_small<UNR, IPT, decltype(sink)&, NoHook, THR>(items, nlive, sink);
     } else if constexpr (COMMIT) {
         tab.commit();
     }

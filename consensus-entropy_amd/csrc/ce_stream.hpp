@@ -163,7 +163,17 @@ __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t b
     sort_stages<64, 32>(k, i);  // half-cleaners 32 .. 1, all best-first
 }
 
-// no-op callback of CommitteeSrc::keys / keys_small (ce_kernels.hpp)
+// item slots a lane keeps in flight in the single-block pools (rows_small).
+// Measured on configs[2] (500 users x 1608, f32): all at once 14.24 us,
+// 1 slot 13.52 us, 2 slots 14.68 us
+// Round 4, after the approximate prefilter (profiles/r04_small_phase_prefilter.json):
+// 1 slot 10.74 us, 2 slots 10.98 us, all 16-23 us (register spills);
+// the last short slot issued with slot 0: C1 6.12 -> 6.42 us, C3 even; the
+// single-pool launches with 2 / all slots in flight: C1 5.86 -> 6.04 / 6.68 us,
+// the mix 6.6 -> 6.92 / 6.94 us.
+constexpr int kSmallThrottle = 1;
+
+// no-op callback of CommitteeSrc::keys / rows_small (ce_kernels.hpp)
 struct NoHook {
     __device__ __forceinline__ void operator()() const {}
 };
