@@ -218,6 +218,16 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
     const int64_t gw = (int64_t)blockIdx.x * 4 + w;
     // grid-cyclic steps (wave g: steps g, g + W, ...; ~1 % over a contiguous run per wave)
     const int64_t lo = gw * G, hi = a.N, step = (int64_t)gridDim.x * 4 * G;
+    // frame-level members in member order (up to 4 read together by the direct path)
+    int nf = 0, f_0 = 0, f_1 = 0, f_2 = 0, f_3 = 0;
+    for (int mm = 0; mm < a.M; ++mm)
+        if (!a.mem[mm].song_level) {
+            f_0 = nf == 0 ? mm : f_0;
+            f_1 = nf == 1 ? mm : f_1;
+            f_2 = nf == 2 ? mm : f_2;
+            f_3 = nf == 3 ? mm : f_3;
+            ++nf;
+        }
     RegTopQ tq;
     tq.init(q);
     for (int64_t t0 = lo; t0 < hi; t0 += step) {
@@ -225,6 +235,66 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
         const bool live = n < hi;
         const int64_t ng = t0 + G < hi ? t0 + G : hi;  // the step's songs [t0, ng)
         double acc = 0.0;  // np.add.reduce identity
+        if (!DMA && nf <= 4) {
+            // direct loads (shuffled frames): each batch's 8 frame indices are
+            // read ONCE for every frame-level member, then all members' rows of
+            // the batch are in flight together (perm read once, 2 serial round
+            // trips per batch instead of 2 per batch and member); each member
+            // keeps its own sequential group sum, and the means meet in member
+            // order below
+            const int64_t f0 = live ? a.off[n] : 0, f1 = live ? a.off[n + 1] : 0;
+            CE_DASSERT(f0 >= 0 && f0 <= f1);
+            constexpr int B = 8;
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+            for (int64_t fb = f0; fb < f1; fb += B) {
+                int64_t r[B];
+#pragma unroll
+                for (int u = 0; u < B; ++u) {
+                    const int64_t f = fb + u < f1 ? fb + u : f1 - 1;
+                    r[u] = a.perm ? a.perm[f] : f;
+                }
+                double v[4][B];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k < nf) {  // wave-uniform
+                        const FrameMember& fm = a.mem[k == 0 ? f_0 : (k == 1 ? f_1 : (k == 2 ? f_2 : f_3))];
+#pragma unroll
+                        for (int u = 0; u < B; ++u) {
+                            const int64_t o = r[u] * fm.ld + c;
+                            v[k][u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
+                                                    : (double)static_cast<const float*>(fm.p)[o];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < B; ++u) {
+                    const bool in = fb + u < f1;
+                    if (nf > 0 && in && v[0][u] == v[0][u]) { s0 += v[0][u]; ++c0; }
+                    if (nf > 1 && in && v[1][u] == v[1][u]) { s1 += v[1][u]; ++c1; }
+                    if (nf > 2 && in && v[2][u] == v[2][u]) { s2 += v[2][u]; ++c2; }
+                    if (nf > 3 && in && v[3][u] == v[3][u]) { s3 += v[3][u]; ++c3; }
+                }
+            }
+            int k = 0;
+            for (int mm = 0; mm < a.M; ++mm) {
+                const FrameMember& fm = a.mem[mm];
+                double mean;
+                if (fm.song_level) {
+                    const int64_t o = (live ? n : t0) * fm.ld + c;
+                    mean = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
+                                         : (double)static_cast<const float*>(fm.p)[o];
+                } else {
+                    const double sk = k == 0 ? s0 : (k == 1 ? s1 : (k == 2 ? s2 : s3));
+                    const int ck = k == 0 ? c0 : (k == 1 ? c1 : (k == 2 ? c2 : c3));
+                    double x = ck ? sk / (double)ck : __longlong_as_double(0x7ff8000000000000ll);
+                    if (fm.dt == kF32) x = (double)(float)x;  // the float32 result column
+                    mean = x;
+                    ++k;
+                }
+                acc += mean;
+            }
+        } else
         for (int mm = 0; mm < a.M; ++mm) {
             const FrameMember& fm = a.mem[mm];
             const int EB = fm.dt == kF64 ? 8 : 4;

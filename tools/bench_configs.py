@@ -266,7 +266,7 @@ def frames_selection_configs(g, report_fn, q=10):
         reps = 200 if songs < 10_000 else 40
         for perm in (None, torch.randperm(F, device="cuda", generator=g)):
             kind = "grouped" if perm is None else "permuted"
-            byts = 3 * F * C * 8 + songs * C * 8 + (3 * F * 8 if perm is not None else 0)
+            byts = 3 * F * C * 8 + songs * C * 8 + (F * 8 if perm is not None else 0)  # the permutation read once
 
             def two_step():
                 for m in range(3):
