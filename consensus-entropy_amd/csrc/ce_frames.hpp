@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
             // order below
             const int64_t f0 = live ? a.off[n] : 0, f1 = live ? a.off[n + 1] : 0;
             CE_DASSERT(f0 >= 0 && f0 <= f1);
-            constexpr int B = 8;
+            constexpr int B = 8;  // (4: 1M songs equal, 1608 songs 38.6 -> 42.4 us)
             double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
             int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
             for (int64_t fb = f0; fb < f1; fb += B) {
