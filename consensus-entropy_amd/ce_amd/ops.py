@@ -307,10 +307,15 @@ def gnb_predict_proba(X, theta, var, class_prior, out=None):
     if tuple(theta.shape) != (C, D) or tuple(var.shape) != (C, D):
         raise ValueError(f"theta/var must be [C, {D}]")
     # np.log(class_prior_[i]) (sklearn 0.24.1 _joint_log_likelihood) with the C
-    # library's log, as numpy 1.19.5 evaluates it: on the host, C values
-    prior = np.asarray(class_prior.cpu() if isinstance(class_prior, torch.Tensor) else class_prior, np.float64)
-    log_prior = torch.tensor([math.log(float(p)) if p > 0 else (-math.inf if p == 0 else math.nan)
-                              for p in prior.reshape(-1)], dtype=torch.float64, device=X.device)
+    # library's log, as numpy 1.19.5 evaluates it: a device prior through the
+    # restated glibc log (ce_log_f64: no host sync, graph-capturable), a host
+    # prior through the C library itself
+    if isinstance(class_prior, torch.Tensor) and class_prior.device == X.device:
+        log_prior = log_f64(class_prior.to(torch.float64).reshape(-1).contiguous())
+    else:
+        prior = np.asarray(class_prior.cpu() if isinstance(class_prior, torch.Tensor) else class_prior, np.float64)
+        log_prior = torch.tensor([math.log(float(p)) if p > 0 else (-math.inf if p == 0 else math.nan)
+                                  for p in prior.reshape(-1)], dtype=torch.float64, device=X.device)
     if out is None:
         out = torch.empty((F, C), dtype=torch.float64, device=X.device)
     call("ce_gnb_predict_proba", _p(X), F, D, X.stride(0), _p(theta), _p(var), _p(log_prior), C, _p(out),

@@ -906,6 +906,22 @@ def test_member_inference_vs_restatement(ce):
     want = ref_gnb_predict_proba(Xt[:3000], gnb.theta_, gnb.var_, prior)
     got = ce.ops.gnb_predict_proba(Xd[:3000], gnb.theta_, gnb.var_, prior).cpu().numpy()
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    # a device prior: log through the restated glibc log on the device (no host
+    # sync), the same bits -- and the call replays from a HIP graph
+    pd_ = dev(prior)
+    got = ce.ops.gnb_predict_proba(Xd[:3000], gnb.theta_, gnb.var_, pd_).cpu().numpy()
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    th, va = dev(gnb.theta_), dev(gnb.var_)
+    out = torch.empty((3000, 4), dtype=torch.float64, device="cuda")
+    ce.ops.gnb_predict_proba(Xd[:3000], th, va, pd_, out=out)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ce.ops.gnb_predict_proba(Xd[:3000], th, va, pd_, out=out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want.view(np.uint64))
     got = ce.ops.sgd_predict_proba(Xd, sgd.coef_, sgd.intercept_).cpu().numpy()
     np.testing.assert_allclose(got, ref_sgd_predict_proba(Xt, sgd.coef_, sgd.intercept_), rtol=1e-10, atol=1e-300)
     # a binary SGD model: [1 - p, p]
