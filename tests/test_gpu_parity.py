@@ -537,6 +537,55 @@ def test_small_pool_single_launch(ce, N):
         assert np.array_equal(idx_np(idx), O.oracle_select_mc(P, q, "NMC")[1]), q
 
 
+@pytest.mark.parametrize("C", [2, 3, 4, 8])
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_small_pool_prefilter_specials(ce, C, dt):
+    """The single-block pools rank by an approximate entropy and evaluate the
+    exact one for survivors only (csrc/ce_small.hpp): rows outside the
+    approximation's domain -- negative, -0.0, NaN, +inf and all-zero means,
+    row sums below 2^-100 or above 2^100 -- must always survive and take the
+    exact path, and near-ties closer than the approximation's error must be
+    ordered by their exact entropies.  One pool, the batched users and (C = 4)
+    the mix, against the oracle."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(100 + C)
+    N, M = 1608, 4
+    P = np.ascontiguousarray(np.transpose(synth(rng, N, M, C, np.float64, quant=0), (1, 0, 2)))  # [M, N, C]
+    base = P[:, 0].copy()
+    k = rng.permutation(N)
+    P[:, k[0:6]] = base[:, None] * (1 + 1e-12 * np.arange(6))[None, :, None]  # near-ties
+    P[:, k[6:9]] = 0.0                       # all-zero rows: NaN entropy, ranked first
+    P[0, k[9:12], 0] = np.nan                # NaN member value
+    P[1, k[12:15], 1 % C] = -0.05            # a negative mean: -inf or NaN entropy
+    P[2, k[15:17], 0] = np.inf               # inf: NaN entropy
+    P[:, k[17:20]] *= 1e-35                  # sums far below 2^-100
+    P[:, k[20:23]] *= 1e35                   # sums far above 2^100
+    P[:, k[23:26]] = -0.0                    # -0.0 everywhere
+    P[:, k[26:29]] *= 1e-300                 # f64-subnormal-range rows (f32: zero rows)
+    P = P.astype(dt)
+    Pn = np.ascontiguousarray(np.transpose(P, (1, 0, 2)))  # [N, M, C]
+    for q in (1, 10, 64):
+        _, idx = ce.ops.select_mc(dev(Pn), q, "NMC")
+        assert np.array_equal(idx_np(idx), O.oracle_select_mc(Pn, q, "NMC")[1]), q
+    # batched: three users over the same rows (specials in each), plus the mix
+    offs = np.array([0, 500, 1100, N], np.int64)
+    ent = O.oracle_committee_entropy(P, "MNC")
+    for q in (10, 64):
+        _, i = ce.ops.select_batched(dev(P), dev(offs), q, "MNC")
+        got = i.cpu().numpy()
+        for u in range(3):
+            exp = O.canonical_order(ent[offs[u]:offs[u + 1]], q)
+            assert np.array_equal(got[u][got[u] >= 0], exp), (u, q)
+    if C == 4:
+        H = Pn[:, 0, :].astype(np.float64).copy()
+        H[k[30:33]] = 0.0
+        q = 10
+        _, i = ce.ops.select_mix(dev(P), dev(H), q, "MNC")
+        want = O.canonical_order(np.concatenate([ent, O.oracle_table_entropy(H)]), q)
+        assert np.array_equal(idx_np(i), want)
+
+
 def test_ticket_counters_return_to_zero(ce):
     """The tiled small-pool kernels and the folded stage 2 draw arrival tickets
     from the workspace header (include/ce.h: zero-filled before first use,
