@@ -347,6 +347,9 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 // Measured and not kept: a 3-deep ring (0.782-0.784 vs
 // 0.790-0.801 of HBM), a 4-wave register cap, the entr pass fed from the LDS
 // row, and 16 KiB LDS-DMA tiles per wave (1.5-2.5 % slower on the C5 job).
+#ifndef CE_WIDE_PREFILTER
+#define CE_WIDE_PREFILTER 1
+#endif
 template <int DT, int KCH, int UNR, int NB = 2>
 __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
@@ -368,6 +371,16 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     const int64_t cnt = a.N > gw ? (a.N - gw + W - 1) / W : 0;
     RegTopQ tq;
     tq.init(q);
+#if CE_WIDE_PREFILTER
+    // a chunked job's running list (sa.extra: the top q of every chunk so far,
+    // best first) bounds this chunk from below: an item not better than its
+    // q-th entry cannot enter the job's top q -- the exact floor, so the
+    // prefilter skips from the first item on
+    if (sa.extra) {
+        const Cand e = sa.extra[q - 1];
+        if (e.idx >= 0 && e.key != 0) tq.init(q, e.key, e.idx);
+    }
+#endif
     const char* base = static_cast<const char*>(a.p);
     const int64_t sNb = a.sN * EB, sMb = a.sM * EB;
     const int K = a.C / CPC;
@@ -398,12 +411,28 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
         X.add(acc);
         if (++cb == NBM) {  // item ci complete
             cb = 0;
-            const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
+            // approximate prefilter (wave-uniform): an item whose approximate
+            // entropy is more than 2 kWideApproxErr2 below the wave's current
+            // threshold (its q-th best exact key, or the running floor) cannot
+            // enter the top q -- its exact entropy is below the threshold -- and
+            // skips the exact entropy (the row sums through LDS, C glibc logs)
+            bool skip = false;
+#if CE_WIDE_PREFILTER
+            if (tq.tk != 0) {
+                bool special;
+                const float ap = wave_approx_entropy<DT, KCH>(acc, K, special);
+                if (!special)
+                    skip = tq.tk == ~0ull ||  // q NaN entropies held: only a NaN ties
+                           (double)ap < key_to_val(tq.tk) * 1.4426950408889634 - 2.0 * kWideApproxErr2;
+            }
+#endif
+            double h = 0.0;
+            if (!skip) h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
 #pragma unroll
             for (int e = 0; e < KCH * CPC; ++e) acc[e] = 0.0;
             const int j = (int)(ci & 63);
             if (lane == j) {
-                mykey = order_key(h);
+                mykey = skip ? 0ull : order_key(h);
                 myidx = lo0 + ci * stride;
             }
             if (j == 63 || ci == cnt - 1) {

@@ -247,6 +247,50 @@ __device__ __forceinline__ double wave_entropy_from_sums(double* acc, int K, dou
     return h;
 }
 
+// The wide stream's approximate prefilter: the approximate entropy (log2
+// units, wave-uniform) of the consensus row whose member sums sit in this
+// wave's registers, from f32 copies (lane sums of KCH*CPC values + a 6-step
+// butterfly, one v_rcp_f32, one v_log_f32 per class).  Error bound for C <=
+// 2048: f32 copy 2^-24, row sum <= 22 roundings, v_rcp_f32 2^-22 -> the
+// quotients' relative error rho <= 1.7e-6; sum_c p_c |log2 p_c| (rho + 2^-21)
+// <= 11 * 2.2e-6, + 2^-20 * sum p_c, + the h sum's <= 22 roundings of <= 11:
+// <= 4e-5 -- kWideApproxErr2 is 5x that.  special: a negative / -0.0 /
+// non-finite sum or a row sum outside [2^-100, 2^100] (the exact path decides).
+constexpr double kWideApproxErr2 = 2e-4;
+template <int DT, int KCH>
+__device__ __forceinline__ float wave_approx_entropy(const double* acc, int K, bool& special) {
+    constexpr int CPC = ChunkT<DT>::CPC;
+    const int lane = threadIdx.x & 63;
+    float mf[KCH * CPC];
+    uint32_t hw = 0;
+    float s = 0.0f;
+#pragma unroll
+    for (int kk = 0; kk < KCH; ++kk) {
+        const bool v = lane + 64 * kk < K;
+#pragma unroll
+        for (int e = 0; e < CPC; ++e) {
+            const double x = v ? acc[kk * CPC + e] : 0.0;
+            const uint32_t h = (uint32_t)(dbits(x) >> 32);
+            hw = hw > h ? hw : h;
+            mf[kk * CPC + e] = (float)x;
+            s += mf[kk * CPC + e];
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);  // same value in every lane
+    special = __ballot(hw >= 0x7ff00000u) != 0 || !(s >= 0x1p-100f && s <= 0x1p100f);
+    const float r = __builtin_amdgcn_rcpf(s);
+    float hl = 0.0f;
+#pragma unroll
+    for (int e = 0; e < KCH * CPC; ++e) {
+        const float pc = __builtin_fmaxf(mf[e] * r, 0x1p-100f);  // absent classes: ~0
+        hl = __builtin_fmaf(-pc, __builtin_amdgcn_logf(pc), hl);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) hl += __shfl_xor(hl, off);
+    return hl;
+}
+
 template <int DT, int KCH, int UNR>
 __device__ inline double wave_item_entropy_vec(const void* p, int64_t off, int M, int C, int64_t sM, double dM,
                                                double invM, bool pow2, const PwPlan& pl, double* row,
