@@ -7,13 +7,14 @@
 //      thread's item slots (item lo + tid + BS*v: each wave's loads coalesced);
 //      each item's exact consensus row (f64 means) is formed as soon as its
 //      own loads have landed, and kept in registers; from it an APPROXIMATE
-//      entropy -- f32 copies, one hardware reciprocal, four hardware log2 --
-//      within kApproxErr2 of the exact one (log2 units), a 32-bit key;
+//      entropy -- f32 copies, one hardware reciprocal, one hardware log2 per
+//      class -- within e = kApproxErr2PerClass * C of the exact one (log2
+//      units; ce_device.hpp), as a 32-bit key;
 //   2. the max approximate key of each group of BS/64 lanes (DPP) -> 64 group
 //      maxima (distinct items) in LDS; every thread counts, for one of them,
 //      the maxima above / not below it over a 1/W slice; the value T of rank
 //      q-1 has q distinct items at or above it;
-//   3. survivors = items whose approximate entropy is >= T - 2 kApproxErr2,
+//   3. survivors = items whose approximate entropy is >= T - 2 e,
 //      plus every "special" row (negative / non-finite means, a sum outside
 //      [2^-100, 2^100]: NaN / -inf entropies and the like, which the
 //      approximation does not cover): a superset of the exact top q (q items
