@@ -1127,6 +1127,47 @@ def test_chunked_pool_vs_oracle(ce, C, dt, N, chunk):
     assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
 
 
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_wide_prefilter_specials(ce, dt):
+    """The wide stream's approximate prefilter (ce_wide.hpp: items whose f32
+    approximate entropy is below the wave's threshold skip the exact entropy;
+    a chunked job seeds the threshold with its running list): near-uniform
+    1000-class rows (most far below the top, so skipped) with a cluster at the
+    top whose entropies differ by far less than the approximation's error,
+    exact duplicates across chunks, and rows the approximation does not
+    cover -- all-zero (NaN entropy), negative, inf, sums far below / above
+    2^+-100 -- in a chunked job and a single call, against the oracle."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(31 if dt == "f32" else 32)
+    N, M, C, chunk = 12_000, 8, 1000, 2_000
+    P = (-np.log(rng.random((N, M, C)))).astype(np.float32)  # spread entropies: most items are skipped
+    k = rng.permutation(N)
+    P[k[20:300]] = 0.5 + 0.01 * rng.random((280, M, C))  # a near-uniform cluster: entropies within ~1e-5
+    P[k[0:6]] = P[k[6]]                       # exact duplicates (lowest position wins)
+    P[k[7:10]] = 0.0                          # NaN entropies: ranked first
+    P[k[10:12], 0, 5] = -1.0                  # a negative mean
+    P[k[12:14], 1, 7] = np.inf
+    P[k[14:16]] *= 1e-32                      # f32 sums below 2^-100
+    P[k[16:18]] *= 1e30                       # f32 sums above 2^100
+    if dt == "bf16":
+        host = _bf16_bits(P)
+        Pd = dev(host.view(np.int16)).view(torch.bfloat16)
+    else:
+        host = P
+        Pd = dev(host)
+    ent_o = O.oracle_committee_entropy(host, "NMC")
+    for q in (1, 10, 64):
+        _, idx_o = O.oracle_topq(ent_o, q)
+        job = ce.ops.MCChunkJob(q, "NMC")
+        for lo in range(0, N, chunk):
+            job.add(Pd[lo:lo + chunk])
+        _, idx = job.result()
+        assert np.array_equal(idx_np(idx), idx_o), q
+        _, idx = ce.ops.select_mc(Pd, q, "NMC")
+        assert np.array_equal(idx_np(idx), idx_o), q
+
+
 def test_c5_full_pool_chunk_invariance(ce):
     """BASELINE configs[4] at its FULL size (50M items x 32 x 1000 bf16, 3.2 TB,
     streamed as the bench streams it: device-generated 250K-item chunks): a
