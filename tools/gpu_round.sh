@@ -10,6 +10,7 @@
 #   PHASE=mpmc       PMC passes over the member kernels (tools/members_pmc.py)
 #   PHASE=small      kernel traces of the small-pool configs + PMC passes of one (tools/small_probe.py)
 #   PHASE=c5         rocprofv3 of the full C5 job (tools/bench_c5.py) + PMC passes at 12M items
+#   PHASE=c5ab       the C5 job at 12M items per library build (ABLIBS="base x"), alternating
 #   PHASE=smallab    small-pool configs under rocprofv3 per library build (LIBS="base reg"), alternating
 #   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
@@ -125,6 +126,15 @@ c5)  # BASELINE configs[4]: rocprofv3 kernel trace of the full 50M x 32 x 1000 b
   timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE -d "$OUT/prof/c5_lds" -o run --output-format csv -- python3 "$ROOT/tools/bench_c5.py" $A > "$OUT/c5_lds.log" 2>&1
   step $? "c5 lds"
   ;;
+c5ab)  # A/B of library builds on the C5 job at 12M items (ABLIBS="base x ..."), builds alternating, 3 reps
+  for rep in 1 2 3; do
+    for lib in ${ABLIBS:-base}; do
+      if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
+      CE_AMD_LIB=$L timeout -k 10 200 python3 tools/bench_c5.py --items ${ITEMS:-12000000} > "$OUT/c5ab_${lib}_$rep.json" 2> "$OUT/c5ab_${lib}_$rep.err"
+      step $? "c5ab $lib $rep"
+    done
+  done
+  ;;
 smallab)  # A/B of library builds on the small-pool configs: kernel traces, builds alternating (LIBS="base reg ...")
   cd /tmp
   for rep in 1 2; do
@@ -153,6 +163,6 @@ firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, debug, phase or firstcall" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase or firstcall" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
