@@ -21,7 +21,8 @@ Also reported:
                 bytes (N_local x 256 B) / its mean duration from HIP events on
                 the launch stream, vs 8 TB/s;
                 traffic = HBM bytes per launch from the committed rocprofv3 PMC
-                pass (profiles/), or null
+                pass (profiles/traffic.json) of the kernel this run launched
+                (ce_last_kernel()), or null when that record names another
   cpu_baseline  the reference's own expressions (amg_test.py:441-445, numpy +
                 scipy) on a bounded sample, rank 0 at N=1 only
 """
@@ -46,11 +47,46 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "pool items scored+ranked/sec (M=16,C=4) at 1/2/4/8 GPUs; % HBM roofline"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
-# the stage-1 kernel each layout launches at M=16, C=4, f32, q <= 64 (ce_kernels.hip launch_stream)
-STAGE1_KERNEL = {
-    "NMC": "ce::k_stream_nmc<f32, C=4, S=16> (item-major, LDS-DMA tiles; stage 2 folded into the last block)",
-    "MNC": "ce::k_stream_nmc<f32, C=4, S=16, member-major> (member-major, LDS-DMA tiles of one 1 KiB run per member; stage 2 folded)",
+# what the stage-1 kernel each layout launches at M=16, C=4, f32, q <= 64 does
+# (csrc/ce_launch_stream.hip); the exact symbol comes from ce_last_kernel()
+STAGE1_ROLE = {
+    "NMC": "item-major [N,M,C], LDS-DMA tiles; stage 2 folded into the last block",
+    "MNC": "member-major [M,N,C], LDS-DMA tiles of one 1 KiB run per member; stage 2 folded",
 }
+
+
+def kernel_symbol(name):
+    """rocprofv3's kernel name without the return type and argument list
+    ("void ce::k<0, 4>(ce::StreamArgs, ...)" -> "ce::k<0, 4>"), the form
+    ce_last_kernel() reports."""
+    name = name.strip()
+    if name.startswith("void "):
+        name = name[5:]
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            return name[:i]
+    return name
+
+
+def recorded_traffic(key, launched):
+    """HBM bytes per launch from profiles/traffic.json for this workload key,
+    only when the profiled kernel is the one this run launched; else None and
+    the reason."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            entry = json.load(f).get(key)
+    except (OSError, ValueError) as e:
+        return None, f"no traffic record ({e!r})"
+    if not entry:
+        return None, f"no traffic record for {key}"
+    if not launched or kernel_symbol(entry["kernel"]) != launched:
+        return None, f"traffic record is for {kernel_symbol(entry['kernel'])}, this run launched {launched or '?'}"
+    return entry["hbm_bytes_per_launch"], entry.get("source")
 
 
 def log(*a):
@@ -142,10 +178,20 @@ def cpu_baseline_multicore(n_items, M, C, q, seed=1987, procs=None):
     n = max(1, n_items // 4)
     env_old = os.environ.get("OMP_NUM_THREADS")
     os.environ["OMP_NUM_THREADS"] = "1"  # inherited by the spawned workers
+    pool = None
     try:
-        with mp.get_context("spawn").Pool(procs) as pool:
-            res = pool.map(ref_mc_shard_time, [(n, M, C, q, seed + 1 + r, 3) for r in range(procs)])
+        pool = mp.get_context("spawn").Pool(procs)
+        res = pool.map(ref_mc_shard_time, [(n, M, C, q, seed + 1 + r, 3) for r in range(procs)])
+        # close + join: the workers exit on their own (Pool.__exit__ would
+        # terminate() them, and under rocprofv3 every SIGTERM'd worker prints
+        # an abort-looking stack)
+        pool.close()
+        pool.join()
+        pool = None
     finally:
+        if pool is not None:  # an exception on the way: do not leave workers behind
+            pool.terminate()
+            pool.join()
         if env_old is None:
             os.environ.pop("OMP_NUM_THREADS", None)
         else:
@@ -287,18 +333,12 @@ def main():
         elapsed = t.item()
     kern_ms = statistics.mean(a.elapsed_time(b) for a, b in ev)
     picks = idx.cpu().tolist()
+    launched = ce_amd._lib.load().ce_last_kernel().decode()  # the stage-1 kernel of the last step
 
     if rank == 0:
         bytes_per_launch = n_local * M * C * P.element_size()
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        try:
-            with open(TRAFFIC_FILE) as f:
-                tr = json.load(f)
-            key = f"{args.layout}_{N}_{M}_{C}_q{q}_w{world}"
-            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
+        traffic, traffic_src = recorded_traffic(f"{args.layout}_{N}_{M}_{C}_q{q}_w{world}", launched)
         line = {
             "metric": METRIC,
             "value": N * args.steps / elapsed,
@@ -325,7 +365,9 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS,
                 "traffic": traffic,
-                "kernel": STAGE1_KERNEL[args.layout],
+                "traffic_source": traffic_src,
+                "kernel": launched,
+                "kernel_role": STAGE1_ROLE[args.layout],
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },

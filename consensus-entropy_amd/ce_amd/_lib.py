@@ -30,6 +30,7 @@ _int, _cstr = ctypes.c_int, ctypes.c_char_p
 SIGNATURES = {
     "ce_last_error": (_cstr, []),
     "ce_version": (_cstr, []),
+    "ce_last_kernel": (_cstr, []),
     "ce_committee_entropy": (_int, [_vp, _int, _i64, _i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
     "ce_vote_entropy": (_int, [_vp, _i64, _i32, _i32, _i64, _vp, _vp, _vp]),
     "ce_va_entropy": (_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
@@ -44,6 +45,7 @@ SIGNATURES = {
     "ce_exp_f64": (_int, [_vp, _i64, _vp, _vp]),
     "ce_exp_f64_host": (_int, [_vp, _i64, _vp]),
     "ce_approx_entropy": (_int, [_vp, _i64, _i32, _vp, _vp, _vp]),
+    "ce_wide_approx_entropy": (_int, [_vp, _i64, _i32, _int, _vp, _vp, _vp]),
     "ce_row_div_f64": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "ce_segment_mean": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _vp, _i64, _vp, _int, _i64, _vp]),
     "ce_select_frames_workspace_bytes": (_sz, [_i64, _i32]),

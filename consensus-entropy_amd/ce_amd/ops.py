@@ -34,11 +34,20 @@ def _on_gpu(t, what):
         raise ValueError(f"{what} must live on a HIP device (got {t.device}); there is no CPU path")
 
 
-def new_workspace(nbytes, device):
-    """A workspace for the engine: zero-filled, as include/ce.h requires (its
+WS_HEADER_BYTES = 65536 + 256  # include/ce.h: the 64 KiB counter header (+ the 256-B alignment carve)
+
+
+def new_workspace(nbytes, device, header_only=False):
+    """A workspace for the engine, zero-filled as include/ce.h requires (its
     header holds the tiled kernels' arrival counters, which every call leaves
-    zero again)."""
-    return torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+    zero again).  header_only: zero just the header -- for the sort path's
+    per-call workspaces, whose body every pass writes before it reads."""
+    n = max(int(nbytes), 256)
+    if not header_only:
+        return torch.zeros(n, dtype=torch.uint8, device=device)
+    buf = torch.empty(n, dtype=torch.uint8, device=device)
+    buf[:WS_HEADER_BYTES].zero_()
+    return buf
 
 
 class _WorkspaceCache:
@@ -47,19 +56,37 @@ class _WorkspaceCache:
     the folded merges, so two streams sharing one would mix their tickets.  A
     buffer grows (never shrinks), so steady state allocates nothing.
 
+    Bounded: at most MAX_STREAMS buffers, least recently used evicted first (a
+    caller cycling through short-lived streams does not pin one buffer per
+    stream; an evicted buffer goes back to torch's allocator in its own
+    stream's order).  Workspaces of the sort path (q > CE_MAX_Q, ~40 B per
+    item: GBs on a 100M pool) are never cached: each such call gets its own,
+    released when the call's tensors are, so one large-q call does not keep
+    them allocated for the life of the process.
+
     Under HIP-graph capture every call gets a FRESH zero-filled workspace
     allocated inside the capture (from the graph's private pool; its zero fill
     is a captured memset that runs at every replay): a graph never references a
     cached buffer, so growing the cache later cannot free memory a graph still
     uses, and replays never share counters with eager calls."""
 
-    def __init__(self):
-        self._ws = {}
+    MAX_STREAMS = 16
 
-    def get(self, device, nbytes):
+    def __init__(self):
+        import collections
+
+        self._ws = collections.OrderedDict()
+
+    def get(self, device, nbytes, transient=False):
         device = torch.device(device)
-        if torch.cuda.is_current_stream_capturing():
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        with torch.cuda.device(device):  # the capture state of THIS device's current stream
+            capturing = torch.cuda.is_current_stream_capturing()
+        if capturing:
             return new_workspace(nbytes, device)
+        if transient:
+            return new_workspace(nbytes, device, header_only=True)
         key = (device.index, torch.cuda.current_stream(device).cuda_stream)
         buf = self._ws.get(key)
         if buf is None or buf.numel() < nbytes:
@@ -67,7 +94,13 @@ class _WorkspaceCache:
             # allocator reuses its block only in this stream's order
             buf = new_workspace(nbytes, device)
             self._ws[key] = buf
+        self._ws.move_to_end(key)
+        while len(self._ws) > self.MAX_STREAMS:
+            self._ws.popitem(last=False)
         return buf
+
+    def __len__(self):
+        return len(self._ws)
 
 
 WORKSPACE = _WorkspaceCache()
@@ -140,6 +173,22 @@ def approx_entropy(rows):
     h2 = torch.empty(n, dtype=torch.float32, device=rows.device)
     sp = torch.empty(n, dtype=torch.uint8, device=rows.device)
     call("ce_approx_entropy", _p(rows), n, C, _p(h2), _p(sp), _stream(rows.device))
+    return h2, sp.bool()
+
+
+def wide_approx_entropy(rows, dtype=torch.bfloat16):
+    """The wide stream's approximate prefilter entropy (ce_wide_approx_entropy:
+    log2 units, f32) of rows [n, C] f64 -- member sums or means, in the register
+    layout k_stream_wide2 uses for a ``dtype`` committee -- and their special
+    flags (verification of the margin the C5 prefilter skips items by)."""
+    _on_gpu(rows, "rows")
+    rows = rows.contiguous()
+    if rows.dtype != torch.float64 or rows.dim() != 2:
+        raise ValueError("wide_approx_entropy takes [n, C] float64")
+    n, C = rows.shape
+    h2 = torch.empty(n, dtype=torch.float32, device=rows.device)
+    sp = torch.empty(n, dtype=torch.uint8, device=rows.device)
+    call("ce_wide_approx_entropy", _p(rows), n, C, _DT[dtype], _p(h2), _p(sp), _stream(rows.device))
     return h2, sp.bool()
 
 
@@ -279,7 +328,7 @@ def select_frames(members, offsets, q, perm=None, base_idx=0, song_level=None):
                              f">= {need}")
         arr[m] = _Member(t.data_ptr(), _DT[t.dtype], 1 if sl else 0, t.stride(0))
     lib = _lib.load()
-    ws = WORKSPACE.get(offsets.device, lib.ce_select_frames_workspace_bytes(N, q))
+    ws = WORKSPACE.get(offsets.device, lib.ce_select_frames_workspace_bytes(N, q), _sort_path(q))
     vals, idx = _outs(q, offsets.device)
     call("ce_select_frames", ctypes.cast(arr, ctypes.c_void_p), len(members), C, _p(offsets), _p(perm), N, q,
          int(base_idx), _p(ws), ws.numel(), _p(vals), _p(idx), _stream(offsets.device))
@@ -381,7 +430,17 @@ def _check_q(q):
     q = int(q)
     if q < 0:
         raise ValueError(f"q={q} is negative")
+    if q > _Q_ABI_MAX:  # every entry point takes q as int32 (ctypes would truncate it silently)
+        raise ValueError(f"q={q} exceeds the C-ABI's int32 q; clamp it to the pool size (min(q, N)) first")
     return q
+
+
+_Q_ABI_MAX = 2**31 - 1
+
+
+def _sort_path(q):
+    """q > CE_MAX_Q runs on the sort path: its workspace is per call (see _WorkspaceCache)."""
+    return q > _lib.CE_MAX_Q
 
 
 def _outs(q, device, lead=()):
@@ -397,7 +456,7 @@ def topq(ent, q, base_idx=0):
     ent = ent.contiguous().to(torch.float64)
     N = ent.numel()
     lib = _lib.load()
-    ws = WORKSPACE.get(ent.device, lib.ce_topq_workspace_bytes(N, q))
+    ws = WORKSPACE.get(ent.device, lib.ce_topq_workspace_bytes(N, q), _sort_path(q))
     vals, idx = _outs(q, ent.device)
     call("ce_topq", _p(ent), N, q, int(base_idx), _p(ws), ws.numel(), _p(vals), _p(idx), _stream(ent.device))
     return vals, idx
@@ -426,7 +485,7 @@ def select_mc(P, q, layout="MNC", base_idx=0, excl=None):
     N, M, C, sN, sM, sC, dt = committee_view(P, layout)
     q = _check_q(q)
     lib = _lib.load()
-    ws = WORKSPACE.get(P.device, lib.ce_select_mc_workspace_bytes(N, q))
+    ws = WORKSPACE.get(P.device, lib.ce_select_mc_workspace_bytes(N, q), _sort_path(q))
     vals, idx = _outs(q, P.device)
     if excl is None:
         call("ce_select_mc", _p(P), dt, N, M, C, sN, sM, sC, q, int(base_idx), _p(ws), ws.numel(), _p(vals),
@@ -567,7 +626,7 @@ class MCChunkJob:
         if N > 0:
             self._ranges.append((base, base + N))
         lib = _lib.load()
-        ws = WORKSPACE.get(P.device, lib.ce_select_mc_chunk_workspace_bytes(N, self.q))
+        ws = WORKSPACE.get(P.device, lib.ce_select_mc_chunk_workspace_bytes(N, self.q), _sort_path(self.q))
         first = 1 if self._fresh else 0
         call("ce_select_mc_chunk", _p(P), dt, N, M, C, sN, sM, sC, self.q, base, _p(self.running), first, _p(ws),
              ws.numel(), _stream(P.device))
@@ -619,7 +678,7 @@ def select_mix(P, hc, q, layout="MNC"):
     q = _check_q(q)
     N_h = hc.shape[0]
     lib = _lib.load()
-    ws = WORKSPACE.get(P.device, lib.ce_select_mix_workspace_bytes(N, N_h, q))
+    ws = WORKSPACE.get(P.device, lib.ce_select_mix_workspace_bytes(N, N_h, q), _sort_path(q))
     vals, idx = _outs(q, P.device)
     call("ce_select_mix", _p(P), dt, N, M, C, sN, sM, sC, _p(hc), N_h, hc.stride(0), q, _p(ws), ws.numel(),
          _p(vals), _p(idx), _stream(P.device))
@@ -637,7 +696,7 @@ def select_batched(P, offsets, q, layout="MNC"):
         raise ValueError("offsets must hold U + 1 >= 2 entries")
     q = _check_q(q)
     lib = _lib.load()
-    ws = WORKSPACE.get(P.device, lib.ce_select_batched_workspace_bytes(N, U, q))
+    ws = WORKSPACE.get(P.device, lib.ce_select_batched_workspace_bytes(N, U, q), _sort_path(q))
     vals, idx = _outs(q, P.device, (U,))
     call("ce_select_batched", _p(P), dt, N, M, C, sN, sM, sC, _p(offsets), U, q, _p(ws), ws.numel(), _p(vals),
          _p(idx), _stream(P.device))

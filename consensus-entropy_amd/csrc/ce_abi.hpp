@@ -6,3 +6,6 @@
 
 CE_HIDDEN int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 CE_HIDDEN int check_launch(const char* what);
+// the kernel the last selection on this thread launched for its main pass, in
+// the demangled form rocprofv3 reports (ce_last_kernel(); "" = none noted)
+CE_HIDDEN void note_kernel(const char* fmt, ...) __attribute__((format(printf, 1, 2)));

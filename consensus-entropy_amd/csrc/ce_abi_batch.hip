@@ -26,6 +26,8 @@ extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, i
     hipStream_t st = (hipStream_t)stream;
     const CommArgs t{hc, kF64, N_h, 1, C, ld_hc, C, 1};  // the hc table: a one-member f64 committee [N_h, 1, C]
     if (q > CE_MAX_Q) {  // entropies of [mc; hc] (positions 0..N-1, N..N+N_h-1), then the sort path
+        rc = check_sort_n(N + N_h);
+        if (rc) return rc;
         const SortWs s = sort_carve(ws, N + N_h);
         rc = launch_entropy(a, nullptr, s.ent, st);
         if (!rc) rc = launch_entropy(t, nullptr, s.ent + N, st);
@@ -101,6 +103,11 @@ extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items
     hipStream_t st = (hipStream_t)stream;
     if (q > CE_MAX_Q) {  // every user's items contiguous in the total order: sort by (user, key, position)
         if (U >= kSortMaxUsers) return fail(CE_EUNSUPPORTED, "q > %d needs U < %d users", CE_MAX_Q, kSortMaxUsers);
+        // a record's position packs (user << kUserShift) | user-local position
+        if (total_items >= (int64_t(1) << kUserShift))
+            return fail(CE_EUNSUPPORTED, "q > %d needs fewer than 2^%d items in all", CE_MAX_Q, kUserShift);
+        rc = check_sort_n(total_items);
+        if (rc) return rc;
         const SortWs s = sort_carve(ws, total_items);
         rc = launch_entropy(a, nullptr, s.ent, st);
         if (rc) return rc;

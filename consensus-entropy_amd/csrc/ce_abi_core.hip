@@ -67,7 +67,17 @@ int check_launch(const char* what) {
     return CE_OK;
 }
 
+static thread_local char g_kernel[256] = "";
+
+void note_kernel(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_kernel, sizeof g_kernel, fmt, ap);
+    va_end(ap);
+}
+
 extern "C" const char* ce_last_error(void) { return g_err; }
+extern "C" const char* ce_last_kernel(void) { return g_kernel; }
 extern "C" const char* ce_version(void) { return "ce_amd 0.1 gfx950"; }
 
 
@@ -152,6 +162,54 @@ extern "C" int ce_approx_entropy(const double* rows, int64_t n, int32_t C, float
         default: return fail(CE_EINVAL, "approx entropy: C must be 2, 3, 4 or 8 (the single-block pools' classes)");
     }
     return check_launch("ce_approx_entropy");
+}
+
+// the wide stream's approximate prefilter (ce_wide.hpp wave_approx_entropy) of n
+// rows [n, C] f64 -- the member sums (or means) of one item each -- laid out in
+// registers as k_stream_wide2<DT, KCH, *> holds them: one wave per row
+template <int DT, int KCH>
+__global__ __launch_bounds__(256) void k_wide_approx(const double* __restrict__ rows, int64_t n, int C,
+                                                     float* __restrict__ h2, uint8_t* __restrict__ special) {
+    constexpr int CPC = ChunkT<DT>::CPC;
+    const int lane = threadIdx.x & 63, K = C / CPC;
+    for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += (int64_t)gridDim.x * 4) {
+        double acc[KCH * CPC];
+#pragma unroll
+        for (int kk = 0; kk < KCH; ++kk) {
+            const int ch = lane + 64 * kk;
+#pragma unroll
+            for (int e = 0; e < CPC; ++e) acc[kk * CPC + e] = ch < K ? rows[i * C + ch * CPC + e] : 0.0;
+        }
+        bool sp;
+        const float a = wave_approx_entropy<DT, KCH>(acc, K, sp);
+        if (lane == 0) {
+            h2[i] = a;
+            special[i] = sp ? 1 : 0;
+        }
+    }
+}
+
+extern "C" int ce_wide_approx_entropy(const double* rows, int64_t n, int32_t C, ce_dtype dt, float* h2,
+                                      uint8_t* special, ce_stream_t stream) {
+    if (n < 0 || (n > 0 && (!rows || !h2 || !special))) return fail(CE_EINVAL, "bad approx-entropy arguments");
+    if (dt != CE_F32 && dt != CE_F64 && dt != CE_BF16) return fail(CE_EINVAL, "bad dtype %d", (int)dt);
+    const int cpc = dt == CE_F32 ? 4 : (dt == CE_F64 ? 2 : 8);
+    if (C < 1 || C > kWideMaxC || C % cpc)
+        return fail(CE_EINVAL, "wide approx entropy: C=%d must be a multiple of %d in [1, %d] (the vector stream's rows)",
+                    C, cpc, kWideMaxC);
+    if (n == 0) return CE_OK;
+    const hipStream_t st = (hipStream_t)stream;
+    const int grid = (int)std::min<int64_t>(cdiv(n, 4), 8192);
+    const int npl = C <= 512 ? 8 : (C <= 1024 ? 16 : 32);  // with_wide_v's per-lane classes
+#define CE_WA(DT_, CPC_)                                                                                       \
+    if ((int)dt == DT_) {                                                                                      \
+        if (npl == 8) hipLaunchKernelGGL((k_wide_approx<DT_, (8 / CPC_ > 0 ? 8 / CPC_ : 1)>), dim3(grid), dim3(256), 0, st, rows, n, C, h2, special); \
+        else if (npl == 16) hipLaunchKernelGGL((k_wide_approx<DT_, 16 / CPC_>), dim3(grid), dim3(256), 0, st, rows, n, C, h2, special); \
+        else hipLaunchKernelGGL((k_wide_approx<DT_, 32 / CPC_>), dim3(grid), dim3(256), 0, st, rows, n, C, h2, special); \
+    }
+    CE_WA(kF32, 4) CE_WA(kF64, 2) CE_WA(kBF16, 8)
+#undef CE_WA
+    return check_launch("ce_wide_approx_entropy");
 }
 
 extern "C" int ce_exp_f64_host(const double* x, int64_t n, double* y) {
@@ -327,6 +385,8 @@ extern "C" int ce_topq(const double* ent, int64_t N, int32_t q, int64_t base_idx
     if (!ws || ws_bytes < ce_topq_workspace_bytes(N, q)) return fail(CE_EWORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
     if (q > CE_MAX_Q) {
+        rc = check_sort_n(N);
+        if (rc) return rc;
         sort_select(sort_carve(ws, N), ent, N, base_idx, nullptr, q, val_out, idx_out, nullptr, st);
         return check_launch("ce_topq");
     }

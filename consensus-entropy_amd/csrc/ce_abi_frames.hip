@@ -49,6 +49,8 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
         double* ent;
         SortWs s{};
         if (q > CE_MAX_Q) {
+            const int rc = check_sort_n(N);
+            if (rc) return rc;
             s = sort_carve(ws, N);
             ent = s.ent;
         } else {

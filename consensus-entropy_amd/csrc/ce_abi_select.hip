@@ -40,8 +40,10 @@ static int mc_partial(const CommArgs& a, int q, int64_t base_idx, const uint32_t
 // q > CE_MAX_Q: entropies into the workspace, then the sort path
 static int mc_sort(const CommArgs& a, const uint32_t* excl, int64_t q, int64_t base_idx, void* ws, double* oval,
                    int64_t* oidx, Cand* ocand, hipStream_t st) {
+    int rc = check_sort_n(a.N);
+    if (rc) return rc;
     const SortWs s = sort_carve(ws, a.N);
-    const int rc = launch_entropy(a, nullptr, s.ent, st);
+    rc = launch_entropy(a, nullptr, s.ent, st);
     if (rc) return rc;
     sort_select(s, s.ent, a.N, base_idx, excl, q, oval, oidx, ocand, st);
     return CE_OK;
@@ -70,6 +72,7 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
                           int64_t sC, const uint32_t* excl, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes,
                           double* val_out, int64_t* idx_out, ce_stream_t stream) {
     hipStream_t st = (hipStream_t)stream;
+    note_kernel("%s", "");
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
     int rc0 = check_comm(a);
     if (rc0) return rc0;

@@ -301,6 +301,16 @@ CE_HIDDEN void rank_merge_lists(const Cand* c, const double* vals, const int64_t
 // ce_abi_core.hip: per-item committee entropy (and optional mean) to HBM, any supported shape
 CE_HIDDEN int launch_entropy(const CommArgs& a, double* mean_or_null, double* ent, hipStream_t st);
 
+// The sort path counts records per wave and per digit in 32 bits
+// (ce_launch_sort.hip): it takes fewer than 2^32 records per call.
+constexpr int64_t kSortMaxRecords = 0xFFFFFFFFll;
+static inline int check_sort_n(int64_t n) {
+    if (n > kSortMaxRecords)
+        return fail(CE_EUNSUPPORTED, "q > %d sorts the pool: it takes < 2^32 items per call (got %lld)", CE_MAX_Q,
+                    (long long)n);
+    return CE_OK;
+}
+
 // entropies ent[0..n) -> the first q slots of the total order (sort path)
 static inline void sort_select(const SortWs& s, const double* ent, int64_t n, int64_t idx0, const uint32_t* excl,
                                int64_t q, double* oval, int64_t* oidx, Cand* ocand, hipStream_t st) {

@@ -377,6 +377,7 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     // q-th entry cannot enter the job's top q -- the exact floor, so the
     // prefilter skips from the first item on
     if (sa.extra) {
+        CE_DASSERT(q >= 1 && q <= kStreamMaxQ);
         const Cand e = sa.extra[q - 1];
         if (e.idx >= 0 && e.key != 0) tq.init(q, e.key, e.idx);
     }

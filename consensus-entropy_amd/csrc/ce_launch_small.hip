@@ -27,6 +27,9 @@ constexpr int small_unr() { return (Src::kC > 4 || BS > 512) ? 2 : 4; }
 template <class SrcA, class SrcB, int IPTA, int IPTB, int BS, int UNRA, bool LONG>
 static void launch_tiles(const SrcA& a, const SrcB& b, const TileArgs& ta, int problems, int q, double* oval,
                          int64_t* oidx, const uint32_t* excl, hipStream_t st) {
+    note_kernel("ce::k_select_tiles<ce::CommitteeSrc<%d, %d, %s>, ce::CommitteeSrc<%d, %d, %s>, %d, %d, %d, 1, %d, %s>",
+                SrcA::kDT, SrcA::kC, SrcA::kVec ? "true" : "false", SrcB::kDT, SrcB::kC, SrcB::kVec ? "true" : "false",
+                IPTA, IPTB, UNRA, BS, LONG ? "true" : "false");
     hipLaunchKernelGGL((k_select_tiles<SrcA, SrcB, IPTA, IPTB, UNRA, 1, BS, LONG>), dim3((unsigned)problems), dim3(BS),
                        0, st, a, b, ta, q, oval, oidx, excl);
 }

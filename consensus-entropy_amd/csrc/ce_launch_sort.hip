@@ -26,6 +26,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const Cand* __restrict__ in, 
     __shared__ uint32_t cnt[4][256];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wv = blockIdx.x * 4 + w;
+    CE_DASSERT(g.chunk % 64 == 0 && (int64_t)g.nw * g.chunk >= g.n);
     for (int d = lane; d < 256; d += 64) cnt[w][d] = 0;
     __builtin_amdgcn_wave_barrier();
     if (wv >= g.nw) return;  // wave-uniform; no block barrier below
@@ -111,6 +112,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const Cand* __restrict__ i
         const uint64_t below = peers & ((1ull << lane) - 1ull);
         uint64_t dst = 0;
         if (ok) dst = next[w][d] + (uint64_t)__popcll(below);
+        CE_DASSERT(!ok || dst < (uint64_t)g.n);
         __builtin_amdgcn_wave_barrier();
         if (ok) {
             out[dst] = c;
@@ -178,6 +180,7 @@ __global__ __launch_bounds__(256) void k_sort_out_users(const Cand* __restrict__
         const int64_t u = t / q, r = t - u * q;
         const int64_t len = offsets[u + 1] - offsets[u];
         const bool ok = r < len;
+        CE_DASSERT(!ok || (offsets[u] >= offsets[0] && len >= 0));
         const Cand c = ok ? s[offsets[u] - offsets[0] + r] : Cand{0ull, -1};
         oval[t] = ok ? key_to_val(c.key) : __longlong_as_double(0x7ff8000000000000ll);
         oidx[t] = ok ? (int64_t)((uint64_t)c.idx & ((1ull << kUserShift) - 1ull)) : -1;

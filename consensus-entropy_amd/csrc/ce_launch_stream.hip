@@ -33,6 +33,7 @@ int launch_stream_fold(const CommArgs& a, int G, int q, int64_t base_idx, WsList
 
 static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                               const uint32_t* excl, const FoldOut* fold) {
+    note_kernel("%s", "");
     if (q > kStreamMaxQ || a.N == 0) return 0;
     StreamArgs sa = stream_args(a, G, base_idx);
     sa.excl = excl;
@@ -52,6 +53,7 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
         auto kern = k_stream_nmc<DT_, C_, S_, 2>;                                                         \
         const int grid = resident_grid(kern, 0, G);                                                       \
+        note_kernel("ce::k_stream_nmc<%d, %d, %d, 2, false>", DT_, C_, S_);                                \
         stream_grid(sa, grid);                                                                            \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                               \
         return folded;                                                                                    \
@@ -69,6 +71,7 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     if (a.dt == DT_ && a.C == C_ && a.M == M_) {                                                       \
         auto kern = k_stream_nmc<DT_, C_, M_, 2, true>;                                                \
         const int grid = resident_grid(kern, 0, G);                                                    \
+        note_kernel("ce::k_stream_nmc<%d, %d, %d, 2, true>", DT_, C_, M_);                              \
         stream_grid(sa, grid);                                                                         \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                            \
         return folded;                                                                                 \
@@ -81,6 +84,8 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
         using S = decltype(src);
         with_batching<S>(a.M, [&](auto unr, auto ipl) {
             auto kern = k_stream_direct<S, decltype(ipl)::value, decltype(unr)::value>;
+            note_kernel("ce::k_stream_direct<ce::CommitteeSrc<%d, %d, %s>, %d, %d>", S::kDT, S::kC,
+                        S::kVec ? "true" : "false", decltype(ipl)::value, decltype(unr)::value);
             const int grid = resident_grid(kern, 0, G);
             stream_grid(sa, grid);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, src, sa, q, w.c);
@@ -100,6 +105,7 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
             // a 2-batch register ring (3 and 4 measured: 72.8 / 71.9 % vs 72.6 % at C5)
             auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
+            note_kernel("ce::k_stream_wide2<%d, %d, %d>", DT, KCH, a.M % UNR == 0 ? UNR : 1);
             const int grid = resident_grid(kern, lds, G);
             stream_grid(sa, grid);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
@@ -111,6 +117,7 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             sa.ctr = nullptr;  // ... and does not fold
             wide_folded = false;
             auto kern = k_stream_wide<DT, NPL, false>;
+            note_kernel("ce::k_stream_wide<%d, %d, false>", DT, NPL);
             const int grid = resident_grid(kern, lds, G);
             stream_grid(sa, grid);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);

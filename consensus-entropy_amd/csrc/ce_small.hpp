@@ -290,6 +290,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
                 for (int v = 0; v < K; ++v) {
                     const int slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(msk[v] >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)msk[v], 0));
+                    CE_DASSERT(slot >= 0);
                     if (pass[v] && slot < SM::CAP) {
 #pragma unroll
                         for (int c = 0; c < C; ++c) sm.sv.m[c][slot] = mrow[v][c];
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
             constexpr int P = C <= 2 ? 2 : (C <= 4 ? 4 : 8);
             constexpr int SPW = 64 / P;
             static_assert(C <= 8, "single-block pools hold rows of <= 8 classes");
+            CE_DASSERT(nc >= 0 && nc + 8 <= SM::CAP + 8);
             if (tid < 8) sm.cs[nc + tid] = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll 1
             for (int t0 = w * SPW; t0 < nc; t0 += W * SPW) {  // wave-uniform
@@ -327,6 +329,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
 #pragma unroll
                 for (int j = 0; j < C; ++j) ee[j] = __shfl(e, (lane & ~(P - 1)) + j);
                 const uint64_t key = order_key(row_sum<C>(ee));
+                CE_DASSERT(ts >= 0 && ts < SM::CAP);
                 if (t < nc && c == 0) sm.cs[t] = make_uint4(sm.sv.nl[t], (uint32_t)key, (uint32_t)(key >> 32), 0u);
             }
             CE_STAMP(blockIdx.x, 5)
@@ -339,12 +342,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
                 // which beat nothing
 #pragma unroll 1
                 for (int j0 = 0; j0 < nc; j0 += 8) {
+                    CE_DASSERT(j0 + 8 <= SM::CAP + 8);  // the zero-padded triples [nc, nc + 8)
                     uint4 a[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) a[k] = sm.cs[j0 + k];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) r = add_if_beats(r, me, a[k]);
                 }
+                CE_DASSERT(i < nc && r >= 0 && r < nc);
                 if (r < q) {
                     ov[r] = key_to_val(((uint64_t)me.z << 32) | me.y);
                     oi[r] = pos_of(~me.x);

@@ -67,6 +67,12 @@ enum {
 
 const char *ce_last_error(void);
 const char *ce_version(void);
+/* The main kernel the last selection call on this thread launched, as
+ * rocprofv3 names it without "void " and the argument list (e.g.
+ * "ce::k_stream_nmc<0, 4, 16, 2, false>"); "" when that call launched none
+ * of the noted kernels.  Lets a benchmark tie a profiled figure to the kernel
+ * it actually ran. */
+const char *ce_last_kernel(void);
 
 /*
  * Per-item committee consensus entropy -- replaces amg_test.py:441 + :443:
@@ -215,6 +221,14 @@ int ce_exp_f64_host(const double *x, int64_t n, double *y);
  * {2, 3, 4, 8}), in log2 units, and whether each row is special (taken by the
  * exact path): verification of the error bound the prefilter's floor relies on. */
 int ce_approx_entropy(const double *rows, int64_t n, int32_t C, float *h2, uint8_t *special, ce_stream_t stream);
+/* The wide stream's approximate prefilter (csrc/ce_wide.hpp wave_approx_entropy:
+ * f32 copies, one v_rcp_f32, a hardware log2 per class) of n rows [n, C] f64 --
+ * member sums or means, laid out as k_stream_wide2 holds a dt committee's rows
+ * in registers (C a multiple of 4 / 2 / 8 for f32 / f64 / bf16, C <= 2048) --
+ * in log2 units, and whether each row is special (taken by the exact path):
+ * verification of the kWideApproxErr2 margin the chunked C5 job skips by. */
+int ce_wide_approx_entropy(const double *rows, int64_t n, int32_t C, ce_dtype dt, float *h2,
+                           uint8_t *special, ce_stream_t stream);
 
 /*
  * Top-q of an entropy vector -- replaces np.argsort(ent)[::-1][:q]

@@ -128,3 +128,55 @@ def test_graph_replay_after_cache_growth(tops):
         g.replay()
         torch.cuda.synchronize()
         assert np.array_equal(_idx(i), _oracle_idx(P, 10))
+
+
+def test_workspace_cache_is_bounded(tops):
+    """The (device, stream) workspace cache keeps at most MAX_STREAMS buffers
+    (least recently used evicted): a caller cycling through short-lived streams
+    does not pin one workspace per stream, and every call still equals the
+    oracle; a sort-path call (q > CE_MAX_Q) gets a per-call workspace that the
+    cache never holds."""
+    import ce_amd.ops as ops
+
+    P = pool(31, (300_000, 16, 4))
+    exp = _oracle_idx(P, 10)
+    torch.cuda.synchronize()
+    n0 = len(ops.WORKSPACE)
+    for _ in range(ops.WORKSPACE.MAX_STREAMS + 8):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            _, i = ops.select_mc(P, 10, "NMC")
+        s.synchronize()
+        assert np.array_equal(_idx(i), exp)
+        assert len(ops.WORKSPACE) <= ops.WORKSPACE.MAX_STREAMS
+    assert len(ops.WORKSPACE) == ops.WORKSPACE.MAX_STREAMS or n0 > ops.WORKSPACE.MAX_STREAMS
+    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream)
+    before = ops.WORKSPACE._ws.get(key)
+    nb = 0 if before is None else before.numel()
+    q = 2049
+    _, iq = ops.select_mc(P, q, "NMC")  # the sort path: ~40 B per item of per-call workspace
+    torch.cuda.synchronize()
+    after = ops.WORKSPACE._ws.get(key)
+    assert (0 if after is None else after.numel()) == nb  # not cached
+    assert np.array_equal(_idx(iq), _oracle_idx(P, q))
+
+
+def test_last_kernel_names_the_stage1_kernel(tops):
+    """ce_last_kernel() names the kernel a selection launched, in rocprofv3's
+    form: bench.py ties its roofline.traffic record to it."""
+    import ce_amd
+    import ce_amd.ops as ops
+
+    lib = ce_amd._lib.load()
+    P = pool(41, (200_000, 16, 4))
+    ops.select_mc(P, 10, "NMC")
+    assert lib.ce_last_kernel().decode() == "ce::k_stream_nmc<0, 4, 16, 2, false>"
+    Pm = P.permute(1, 0, 2).contiguous()
+    ops.select_mc(Pm, 10, "MNC")
+    assert lib.ce_last_kernel().decode() == "ce::k_stream_nmc<0, 4, 16, 2, true>"
+    small = pool(42, (4, 1608, 4))
+    ops.select_mc(small, 10, "MNC")
+    assert lib.ce_last_kernel().decode().startswith("ce::k_select_tiles<ce::CommitteeSrc<0, 4, true>")
+    ops.select_mc(P, 100, "NMC")  # q > 64: the block-synchronous lists, not a noted kernel
+    assert lib.ce_last_kernel().decode() == ""
+    torch.cuda.synchronize()

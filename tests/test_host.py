@@ -149,3 +149,74 @@ def test_any_q_without_gpu():
     ws = lib.ce_select_mc_workspace_bytes(N, 10)  # big enough for the lists, not for the sort
     assert lib.ce_select_mc(p, 0, N, 16, 4, 64, 4, 1, big, 0, p, ws, p, p, None) == _lib.CE_EWORKSPACE
     assert lib.ce_select_mc(p, 0, N, 16, 4, 64, 4, 1, -5, 0, p, ws, p, p, None) == _lib.CE_EINVAL
+
+
+def test_sort_path_rejects_2pow32_records_without_gpu():
+    """The radix sort counts records in 32 bits (ce_launch_sort.hip): a pool of
+    2^32 items or more with q > CE_MAX_Q is refused, not mis-sorted; batched
+    users pack (user << 40 | position) and refuse 2^40 items."""
+    from ce_amd import _lib
+
+    lib = _lib.load()
+    p = ctypes.c_void_p(256)
+    q = _lib.CE_MAX_Q + 1
+    big = 1 << 32
+    huge_ws = (1 << 63) - 1
+    rc = lib.ce_topq(p, big, q, 0, p, huge_ws, p, p, None)
+    assert rc == _lib.CE_EUNSUPPORTED and b"2^32" in lib.ce_last_error()
+    rc = lib.ce_select_mc(p, 0, big, 16, 4, 64, 4, 1, q, 0, p, huge_ws, p, p, None)
+    assert rc == _lib.CE_EUNSUPPORTED
+    rc = lib.ce_select_mc_cands(p, 0, big, 16, 4, 64, 4, 1, q, 0, p, huge_ws, p, None)
+    assert rc == _lib.CE_EUNSUPPORTED
+    rc = lib.ce_select_mix(p, 0, big - 5, 4, 4, 16, 4, 1, p, 10, 4, q, p, huge_ws, p, p, None)
+    assert rc == _lib.CE_EUNSUPPORTED
+    rc = lib.ce_select_batched(p, 0, 1 << 40, 4, 4, 16, 4, 1, p, 8, q, p, huge_ws, p, p, None)
+    assert rc == _lib.CE_EUNSUPPORTED and b"2^40" in lib.ce_last_error()
+
+
+def test_q_beyond_int32_is_rejected():
+    """Every entry point takes q as int32: ops refuses a larger q instead of
+    letting ctypes truncate it."""
+    pytest.importorskip("torch")
+    from ce_amd import ops
+
+    assert ops._check_q(2**31 - 1) == 2**31 - 1
+    with pytest.raises(ValueError, match="int32"):
+        ops._check_q(2**32 + 3)
+    with pytest.raises(ValueError, match="negative"):
+        ops._check_q(-1)
+
+
+def test_bench_traffic_only_for_the_launched_kernel(tmp_path, monkeypatch):
+    """bench.py's roofline.traffic comes from profiles/traffic.json only when
+    the record names the kernel this run launched (ce_last_kernel())."""
+    import json
+
+    import bench
+
+    sym = "void ce::k_stream_nmc<0, 4, 16, 2, false>(ce::StreamArgs, int, ce::Cand*)"
+    assert bench.kernel_symbol(sym) == "ce::k_stream_nmc<0, 4, 16, 2, false>"
+    assert bench.kernel_symbol("ce::k<a<(1)>, 2>") == "ce::k<a<(1)>, 2>"
+    path = tmp_path / "traffic.json"
+    path.write_text(json.dumps({"NMC_k": {"kernel": sym, "hbm_bytes_per_launch": 123.0, "source": "x"}}))
+    monkeypatch.setattr(bench, "TRAFFIC_FILE", str(path))
+    assert bench.recorded_traffic("NMC_k", "ce::k_stream_nmc<0, 4, 16, 2, false>") == (123.0, "x")
+    t, why = bench.recorded_traffic("NMC_k", "ce::k_stream_nmc<0, 4, 16, 2, true>")
+    assert t is None and "this run launched" in why
+    assert bench.recorded_traffic("NMC_k", "")[0] is None
+    assert bench.recorded_traffic("MNC_k", "ce::k_stream_nmc<0, 4, 16, 2, false>")[0] is None
+
+
+def test_committed_traffic_records_name_a_kernel():
+    """Every committed traffic record names its exact kernel symbol and source profile."""
+    import json
+    import os
+
+    from conftest import ROOT
+
+    tr = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+    assert tr
+    for key, e in tr.items():
+        assert e["kernel"].startswith("void ce::k_") and "(" in e["kernel"], key
+        assert e["hbm_bytes_per_launch"] > 0 and e["source"].startswith("profiles/"), key
+        assert "k_stream_direct" not in e["kernel"], key

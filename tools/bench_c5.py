@@ -76,7 +76,8 @@ def run(items=50_000_000, chunk=2_000_000, members=32, classes=1000, q=10, log=T
         "items": items, "chunks": nch, "n_gpus": world, "score_s": score_s, "items_per_s": items / score_s,
         "GB_per_s": nbytes / score_s / 1e9, "frac_hbm": nbytes / score_s / 1e9 / PEAK / world,
         "wall_s_incl_generation": wall,
-        "selected": idx.cpu().tolist(), "entropies": vals.cpu().tolist()}
+        "selected": idx.cpu().tolist(), "entropies": vals.cpu().tolist(),
+        "entropy_bits": [f"{b & 0xFFFFFFFFFFFFFFFF:016x}" for b in vals.view(torch.int64).cpu().tolist()]}
 
 
 def main():
@@ -88,6 +89,7 @@ def main():
     ap.add_argument("--members", type=int, default=32)
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--q", type=int, default=10)
+    ap.add_argument("--quiet", action="store_true")
     a = ap.parse_args()
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
@@ -95,7 +97,7 @@ def main():
         from ce_amd import dist as cdist
 
         cdist.init("nccl", device=torch.device("cuda", torch.cuda.current_device()))
-    line = run(a.items, a.chunk, a.members, a.classes, a.q, rank=rank, world=world)
+    line = run(a.items, a.chunk, a.members, a.classes, a.q, log=not a.quiet, rank=rank, world=world)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

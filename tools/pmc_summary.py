@@ -59,7 +59,8 @@ for layout in ("NMC", "MNC"):
         k = stage1[0]
         key = f"{layout}_100000000_16_4_q10_w1"
         traffic[key] = {"kernel": k, "hbm_bytes_per_launch": pmc[k]["hbm_bytes_per_launch"],
-                        "fetch_KiB": pmc[k].get("FETCH_SIZE_KiB_mean"), "write_KiB": pmc[k].get("WRITE_SIZE_KiB_mean"),
+                        "fetch_bytes": pmc[k].get("FETCH_SIZE_KiB_mean", 0.0) * 1024 * 2,
+                        "write_bytes": pmc[k].get("WRITE_SIZE_KiB_mean", 0.0) * 1024,
                         "source": f"profiles/{tag}_{layout}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"}
     print(layout, json.dumps(pmc, indent=1)[:1500])
 # secondary configs (tools/bench_configs.py): stats of every kernel, PMC of the wide stream

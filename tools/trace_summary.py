@@ -55,6 +55,20 @@ out = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1
        "bench_line": bench, "ms_per_step": bench["ms_per_step"], "kernels": kern,
        "note": "timed_* = the last `steps` dispatches (the timed region); all_* include the warm-up dispatches"}
 json.dump(out, open(os.path.join(out_dir, f"{tag}_bench_exact.json"), "w"), indent=1)
+# bench.py's roofline.traffic: the PMC of the stage-1 kernel this command launched
+stage1 = [k for k in kern if "k_stream" in k and "hbm_bytes_per_launch_pmc" in kern[k]]
+if stage1:
+    k = stage1[0]
+    traffic_path = os.path.join(out_dir, "traffic.json")
+    traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
+    cfg = bench["config"]
+    key = f"{cfg['layout']}_{cfg['n_items']}_{cfg['members']}_{cfg['classes']}_q{cfg['q']}_w{bench['n_gpus']}"
+    traffic[key] = {"kernel": k, "hbm_bytes_per_launch": kern[k]["hbm_bytes_per_launch_pmc"],
+                    "fetch_bytes": kern[k]["fetch_bytes_per_launch_pmc"],
+                    "write_bytes": kern[k]["write_bytes_per_launch_pmc"],
+                    "source": f"profiles/{tag}_bench_exact.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                              f"bench.py; FETCH x 2 per the gfx950 rule + WRITE)"}
+    json.dump(traffic, open(traffic_path, "w"), indent=1)
 rows = list(csv.reader(open(os.path.join(tdir, "run_kernel_stats.csv"))))
 head, body = rows[0], rows[1:]
 body.sort(key=lambda r: (not r[0].startswith("void ce::"), -float(r[2])))
