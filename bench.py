@@ -12,7 +12,8 @@ top-q with one RCCL all-gather before an identical merge on every rank.
 One step = the full selection: ONE kernel per rank -- fused score + per-block
 top-q over the resident shard (the streaming stage 1) whose last block merges
 the blocks' candidates (stage 2 folded in) -- and for N > 1 the all-gather of
-every rank's q candidate records (16 B each) + the merge.  Inputs are synthetic
+every rank's q candidate records (16 B each) + the merge
+(ce_amd.dist.ShardedStep).  Inputs are synthetic
 Dirichlet(1) member rows (1% un-normalised, like sigmoid CNN members), seed
 1987, generated on the device before timing.
 
@@ -285,44 +286,41 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] pool shard {n_local} x {M} x {C} fp32 ({P.numel() * 4 / 1e9:.1f} GB) "
         f"generated in {time.time() - t0:.1f}s")
-    plan = ops.MCPlan(P, q, args.layout, base_idx=lo)
-    # N > 1: stage 2 writes this rank's q candidate records (ce_cand, 16 B each)
-    # straight into the all-gather send buffer; the merge reads the receive
-    # buffer as is -- per step: stage 1, stage 2, one RCCL all-gather, merge.
-    send = torch.empty((q, 2), dtype=torch.int64, device=device)
-    recv = torch.empty((world * q, 2), dtype=torch.int64, device=device)
-
-    def local():
-        """This rank's selection kernel: ONE launch (stage 2 folded into the
-        streaming stage 1's last block) -> final (vals, idx) at N = 1, the
-        rank's q candidate records (the all-gather send buffer) at N > 1."""
-        if world == 1:
-            return plan.step()
-        if q > 64:  # records need q <= 64: exchange packed (entropy, position) pairs instead
-            return plan.step()
-        return plan.step_cands(send)
-
-    def exchange(loc):
-        if world == 1:
-            return loc
-        if q > 64:
-            return ops.topq_merge(*cdist.allgather_topq(*loc, q), q)
-        cdist.allgather_cands(send, out=recv)
-        return ops.merge_cands(recv, q)
-
-    for _ in range(args.warmup):
-        exchange(local())
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world == 1 or q > 64:
+        plan = ops.MCPlan(P, q, args.layout, base_idx=lo)
+
+        def step(k):
+            """N = 1: ONE launch (stage 2 folded into the streaming stage 1's
+            last block) -> the final (vals, idx).  N > 1 with q > 64: the rank's
+            list, then the packed (entropy, position) exchange and merge."""
+            if k >= 0:
+                ev[k][0].record(stream)
+            loc = plan.step()
+            if k >= 0:
+                ev[k][1].record(stream)
+            if world == 1:
+                return loc
+            return ops.topq_merge(*cdist.allgather_topq(*loc, q), q)
+    else:
+        # N > 1: stage 1 (stage 2 folded in) writes this rank's q candidate
+        # records (ce_cand, 16 B each) straight into the all-gather send buffer,
+        # one RCCL all-gather, the merge of the receive buffer (eager: a HIP
+        # graph of the step measured slower, ce_amd.dist.ShardedStep)
+        sstep = cdist.ShardedStep(P, q, global_offset=lo, layout=args.layout)
+
+        def step(k):
+            return sstep(ev[k] if k >= 0 else None)
+
+    for _ in range(args.warmup):
+        step(-1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
-        loc = local()
-        ev[k][1].record(stream)
-        vals, idx = exchange(loc)
+        vals, idx = step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -379,7 +377,7 @@ def main():
                                  "note": "NOT a multi-GPU measurement"}
             line["value"] = None
         if world == 1 and not args.no_cpu_baseline:
-            del P, plan
+            del P, plan, step
             torch.cuda.empty_cache()
             line["cpu_baseline"] = cpu_baseline(args.cpu_sample, M, C, q)
         print(json.dumps(line), flush=True)

@@ -98,6 +98,77 @@ def allgather_cands(cands, group=None, out=None):
     return out
 
 
+class ShardedStep:
+    """One rank's step of the sharded mc selection, as bench.py runs it every
+    step: stage 1 with stage 2 folded in (ONE kernel writing this rank's q
+    records into the all-gather send buffer), the all-gather of every rank's
+    records, and the merge of the receive buffer.
+
+    The step runs eagerly: the host enqueues the all-gather and the merge while
+    the stage-1 kernel runs, so on the GPU they follow it within ~5 us at the
+    8-GPU shard size (profiles/r05_scale_proxy.json, world-1 RCCL).  capture()
+    records the step as one HIP graph instead (RCCL collectives are
+    graph-capturable; gloo's are not: it declines on any other backend); it is
+    kept as an option and tested, but measured SLOWER on MI355X -- a replay
+    added ~24 us over the kernel against the eager step's ~5 us -- so bench.py
+    does not use it.
+
+    Output: (vals [q], idx [q]) tensors (the graph's outputs when captured,
+    overwritten by every replay)."""
+
+    def __init__(self, P_local, q, *, global_offset, layout="NMC", group=None):
+        if not 1 <= int(q) <= 64:
+            raise ValueError("ShardedStep takes 1 <= q <= 64 (the one-launch record path); "
+                             "use sharded_select_mc for larger q")
+        self.q = int(q)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.plan = ops.MCPlan(P_local, self.q, layout, base_idx=int(global_offset))
+        self.device = P_local.device
+        self.send = torch.empty((self.q, 2), dtype=torch.int64, device=self.device)
+        self.recv = torch.empty((self.world * self.q, 2), dtype=torch.int64, device=self.device)
+        self.graph = None
+        self.out = None
+
+    def eager(self, ev=None):
+        """The step without a graph; ev = (e0, e1) HIP events around the stage-1 kernel."""
+        if ev is not None:
+            ev[0].record()
+        self.plan.step_cands(self.send)
+        if ev is not None:
+            ev[1].record()
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+            return ops.merge_cands(self.recv, self.q)
+        return ops.merge_cands(self.send, self.q)
+
+    def capture(self, warmup=2):
+        """Capture the step as one HIP graph, after `warmup` eager steps on a
+        side stream (torch's capture rules).  Returns False -- the step stays
+        eager -- when the backend's collective cannot be captured."""
+        if self.world > 1 and dist.get_backend(self.group) != "nccl":
+            return False
+        cur = torch.cuda.current_stream(self.device)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.eager()
+        cur.wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.out = self.eager()
+        self.graph = g
+        return True
+
+    def __call__(self, ev=None):
+        if self.graph is not None:
+            self.graph.replay()
+            return self.out
+        return self.eager(ev)
+
+
 def sharded_select_mc_records(P_local, q, *, global_offset, layout="NMC", group=None, local_records=None,
                               merge_records=None):
     """sharded_select_mc over the record exchange (any q): stage 1 + stage 2

@@ -60,6 +60,50 @@ def test_rccl_record_exchange_world1():
         dist.destroy_process_group()
 
 
+def test_rccl_step_graph_world1():
+    """bench.py's N > 1 step (ce_amd.dist.ShardedStep: stage 1 with stage 2
+    folded into this rank's records, the RCCL all-gather, the merge) on a
+    world-1 RCCL group, eager and captured as a HIP graph: every replay equals
+    the eager step and the oracle, also after the pool changes in place."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import torch.distributed as dist
+
+    import ce_amd
+    from ce_amd import dist as cdist
+    from oracle import ce_oracle as O
+
+    ce_amd.load()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(6)
+        e = -np.log(rng.random((300_007, 16, 4)))
+        P = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+        Pd = torch.from_numpy(P).cuda()
+        step = cdist.ShardedStep(Pd, 10, global_offset=5)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        v0, i0 = step(ev)
+        torch.cuda.synchronize()
+        assert ev[0].elapsed_time(ev[1]) > 0
+        exp = O.oracle_select_mc(P, 10, "NMC")[1] + 5
+        assert np.array_equal(i0.cpu().numpy(), exp)
+        v0, i0 = v0.clone(), i0.clone()
+        assert step.capture()
+        for _ in range(4):
+            v, i = step()
+            torch.cuda.synchronize()
+            assert torch.equal(i, i0) and torch.equal(v.view(torch.int64), v0.view(torch.int64))
+        e2 = -np.log(rng.random(P.shape))
+        P2 = (e2 / e2.sum(-1, keepdims=True)).astype(np.float32)
+        Pd.copy_(torch.from_numpy(P2))
+        _, i2 = step()
+        torch.cuda.synchronize()
+        assert np.array_equal(i2.cpu().numpy(), O.oracle_select_mc(P2, 10, "NMC")[1] + 5)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_bench_contract_small():
     """bench.py's JSON line (the driver's contract) on a small pool: the
     required keys, roofline / cpu_baseline objects, and a selection that

@@ -333,6 +333,65 @@ def test_approx_entropy_bound(ce):
     print("max |approx - exact| (log2 units) per C:", worst)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_wide_approx_entropy_bound(ce, dtype):
+    """The C5 stream's prefilter (csrc/ce_wide.hpp wave_approx_entropy) skips an
+    item only when its f32 approximate entropy is more than 2 * kWideApproxErr2
+    (log2 units) below the threshold; that never drops a top-q item if the
+    device approximation stays within kWideApproxErr2 of the exact entropy.
+    Measured here on >= 1.1e6 wide rows per dtype layout -- Dirichlet from very
+    peaked to near-uniform, zero classes, classes down to 1e-300, unnormalised
+    rows with sums from 2^-90 to 2^90, C in {16, 136, 1000, 2048} (the vector
+    stream's row widths; C = 129 has no vector path and never prefilters) --
+    against the exact device entropy (glibc log, bit-equal to scipy), with a
+    4x margin; rows that must take the exact path (negative, -0.0, NaN, inf,
+    sums outside [2^-100, 2^100]) are flagged special."""
+    kWideApproxErr2 = 2e-4  # csrc/ce_wide.hpp
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    g = torch.Generator(device="cuda").manual_seed(505)
+    worst, n_rows = {}, 0
+    for C in (16, 136, 1000, 2048):
+        per = 300_000 if C <= 136 else 40_000
+        parts = []
+        for a in (0.02, 0.2, 1.0, 5.0, 100.0):
+            gam = torch._standard_gamma(torch.full((per, C), a, dtype=torch.float64, device="cuda"), generator=g)
+            parts.append(gam / gam.sum(1, keepdim=True))
+        base = parts[2]
+        z = base.clone()
+        z[torch.rand(z.shape, generator=g, device="cuda", dtype=torch.float64) < 0.3] = 0.0
+        parts.append(z)  # zero classes
+        t = base.clone()
+        t[:, 0] = 10.0 ** (torch.rand(per, generator=g, device="cuda", dtype=torch.float64) * -280 - 20)
+        parts.append(t)  # tiny classes
+        u = base * (2.0 ** ((torch.rand((per, 1), generator=g, device="cuda", dtype=torch.float64) - 0.5) * 180))
+        parts.append(u)  # unnormalised member sums, 2^-90 .. 2^90
+        v = torch.full((per, C), 1.0 / C, dtype=torch.float64, device="cuda")
+        v += torch.randn((per, C), generator=g, device="cuda", dtype=torch.float64) * (1e-7 / C)
+        parts.append(v.abs())  # near-uniform
+        R = torch.cat(parts)
+        h2, spec = ce.ops.wide_approx_entropy(R, tdt)
+        assert not bool(spec.any()), C
+        exact = ce.ops.committee_entropy(R.view(R.shape[0], 1, C), "NMC") / np.log(2.0)
+        err = (h2.double() - exact).abs()
+        worst[C] = float(err.max())
+        n_rows += R.shape[0]
+        assert worst[C] <= kWideApproxErr2 / 4, (C, worst[C])
+        # rows the approximation does not cover are flagged (the exact path decides them)
+        sp = base[:8].clone().repeat(8, 1)
+        sp[0:8, 0] = -sp[0:8, 0]
+        sp[8:16, 1] = float("nan")
+        sp[16:24, 2] = float("inf")
+        sp[24:32, 3] = -0.0
+        sp[32:40] *= 2.0 ** -110
+        sp[40:48] *= 2.0 ** 110
+        sp[48:56] = 0.0
+        _, spf = ce.ops.wide_approx_entropy(sp, tdt)
+        assert bool(spf[:56].all()) and not bool(spf[56:].any()), C
+        del parts, R, base, z, t, u, v
+    assert n_rows >= 1_100_000
+    print(f"{dtype}: max |approx - exact| (log2 units) per C:", worst)
+
+
 def test_row_division_bit_exact(ce):
     """The entropy's row division (one shared reciprocal per row, exact by
     construction -- DESIGN.md 'Numerics') equals IEEE x / s on 6e7 pairs:
@@ -1197,3 +1256,48 @@ def test_c5_full_pool_chunk_invariance(ce):
     v1, i1 = ce.ops.select_mc(buf, q, "NMC", base_idx=c0 * nc)
     assert int(i1[0].item()) == int(ia[0].item())
     assert v1[0].view(torch.int64).item() == va[0].view(torch.int64).item()
+
+
+def _bench_c5_child(lib, items, chunk, q):
+    """tools/bench_c5.py in a child process on library build `lib` (None: the
+    product library): the job's q positions and entropy bits."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("CE_AMD_LIB", None)
+    if lib:
+        env["CE_AMD_LIB"] = lib
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "bench_c5.py"), "--items", str(items), "--chunk",
+                        str(chunk), "--q", str(q), "--quiet"], cwd=root, capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    return line["selected"], line["entropy_bits"], line["frac_hbm"]
+
+
+@pytest.mark.parametrize("items,q", [(50_000_000, 10), (12_000_000, 64)])
+def test_c5_prefilter_pinned_full_size(ce, items, q):
+    """The C5 job's approximate prefilter (an item whose f32 approximate entropy
+    lies more than 2 * kWideApproxErr2 below the running threshold skips its
+    exact entropy) pinned at full size against the exact path: the same
+    device-generated 2M-item chunks (BASELINE configs[4]: 32 members x 1000
+    bf16 classes; at 50M items the whole 3.2 TB pool) scored by the product
+    library and by the build without the prefilter
+    (tools/_diag/libce_amd_noprefilter.so, `make noprefilter`, built by
+    __graft_entry__.build()) -- where nearly every item skips -- must give
+    every one of the q positions and their entropy bits identically
+    (amg_test.py:441-445)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exact_lib = os.path.join(root, "tools", "_diag", "libce_amd_noprefilter.so")
+    assert os.path.exists(exact_lib), "build the exact-path reference first: make -C consensus-entropy_amd noprefilter"
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # the children need a 128 GB chunk each
+    sel_p, bits_p, frac_p = _bench_c5_child(None, items, 2_000_000, q)
+    sel_e, bits_e, frac_e = _bench_c5_child(exact_lib, items, 2_000_000, q)
+    assert len(sel_p) == q and min(sel_p) >= 0 and max(sel_p) < items
+    assert sel_p == sel_e
+    assert bits_p == bits_e
+    print(f"items={items} q={q}: prefiltered {frac_p:.3f} vs exact path {frac_e:.3f} of HBM")

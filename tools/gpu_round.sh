@@ -15,6 +15,8 @@
 #   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
+#   PHASE=scale      tools/scale_proxy.py (per-rank proxies; world-1 RCCL step eager vs HIP graph)
+#   PHASE=tests      selected GPU tests (TESTS=files, TESTK=-k expression, PYTEST_ARGS=...)
 # Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -159,10 +161,18 @@ phase)  # per-block phase stamps of the C3 selection (tools/phase_probe.py) on t
     done
   done
   ;;
+scale)  # single-GPU proxies of one rank at 1/2/4/8 GPUs + the world-1 RCCL step, eager vs HIP graph (tools/scale_proxy.py)
+  timeout -k 10 300 python3 tools/scale_proxy.py > "$OUT/scale_proxy.json" 2> "$OUT/scale_proxy.err"
+  step $? "scale proxy"
+  ;;
+tests)  # selected GPU tests only: TESTS="file::name ..." or PYTEST_ARGS="-k expr" (failures keep going)
+  timeout -k 10 ${TLIM:-600} python -u -m pytest ${TESTS:-tests} -m gpu -v -s --timeout 400 --timeout-method thread ${TESTK:+-k "$TESTK"} ${PYTEST_ARGS} > "$OUT/pytest_sel.log" 2>&1
+  step $? "pytest selected"
+  ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase or firstcall" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale or tests" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"

@@ -6,6 +6,8 @@ kernel on one shape):
   c2mix configs[1]  mix [4 x 1608 x 4 f32 ; 1608 x 4 hc]
   c3    configs[2]  500 users x 4 x 1608 x 4 f32, one launch (dense)
   c3r   configs[2]  the ragged variant (N_u in [128, 1608])
+  c3cold configs[2] dense, rotating 8 distinct 51.5 MB pools between launches
+        (412 MB > the 256 MiB Infinity Cache: each launch reads its pool from HBM)
   python tools/small_probe.py c3 [reps]"""
 import os
 import sys
@@ -36,6 +38,15 @@ def make(cfg, g):
     if cfg == "c3":
         offs = torch.arange(0, U + 1, device="cuda", dtype=torch.int64) * Nu
         return lambda: ops.select_batched(P, offs, q, "MNC")
+    if cfg == "c3cold":
+        offs = torch.arange(0, U + 1, device="cuda", dtype=torch.int64) * Nu
+        pools = [P] + [dirichlet((4, U * Nu, 4), torch.float32, g) for _ in range(7)]
+        it = [0]
+
+        def call():
+            it[0] += 1
+            return ops.select_batched(pools[it[0] % len(pools)], offs, q, "MNC")
+        return call
     if cfg == "c3r":
         sizes = torch.randint(128, 1609, (U,), generator=torch.Generator().manual_seed(1987))
         offs = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(sizes, 0)]).cuda()
