@@ -42,16 +42,6 @@
 
 namespace ce {
 
-// Tail variants (A/B builds: make variant-small DEFS=...): CE_SMALL_FLOOR1 --
-// the floor's counts in one barrier; CE_SMALL_OWN_EXACT -- every thread
-// evaluates its own survivors' exact keys (no LDS row hand-off to wave 0).
-#ifndef CE_SMALL_FLOOR1
-#define CE_SMALL_FLOOR1 0
-#endif
-#ifndef CE_SMALL_OWN_EXACT
-#define CE_SMALL_OWN_EXACT 0
-#endif
-
 #ifdef CE_PHASE_TIMING
 // diagnostic build only (-DCE_PHASE_TIMING): per-block wall-clock stamps (100 MHz)
 // [0] start, [1] wave 0's keys done, [2] floor, [3] append, [4] rank, [5] exact keys (wave 0),
@@ -194,12 +184,6 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
     LogTablePrefetch tab;
     tab.fetch();
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-#if CE_SMALL_OWN_EXACT
-    // the survivors' triples land in cs[0, nc); cs[nc, nc + 8) must read as zero
-    // triples (they beat nothing) for the 8-wide rank reads: zero all of cs now,
-    // while the block's first loads are in flight
-    for (int i = tid; i < SM::CAP + 8; i += BS) sm.cs[i] = make_uint4(0u, 0u, 0u, 0u);
-#endif
     const int p = blockIdx.x;
     const int64_t lo = ta.offsets ? ta.offsets[p] : 0, hi0 = ta.offsets ? ta.offsets[p + 1] : ta.n;
     const int64_t hi = hi0 > lo ? hi0 : lo;
@@ -259,16 +243,6 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
         if (tid == 0) sm.cnt = 0;
         __syncthreads();
         const uint32_t mg = sm.gm[lane];
-#if CE_SMALL_FLOOR1
-        // every wave counts, for the maximum its lane holds, all 64 maxima above /
-        // not below it (64 broadcast LDS reads): no partial counts, no 2nd barrier
-        int r = 0;
-#pragma unroll
-        for (int j = 0; j < 64; ++j) {
-            const uint32_t o = sm.gm[j];
-            r += (o > mg ? 1 : 0) + (o >= mg ? 0x10000 : 0);
-        }
-#else
         {
             int r = 0;
 #pragma unroll
@@ -279,14 +253,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
             sm.part[w][lane] = r;
         }
         __syncthreads();
-#endif
         uint32_t thr;  // survivors: approximate key >= thr (>= 1: never a slot without an item)
         {
-#if !CE_SMALL_FLOOR1
             int r = 0;
 #pragma unroll
             for (int j = 0; j < W; ++j) r += sm.part[j][lane];
-#endif
             const int above = r & 0xffff, notbelow = r >> 16;
             const int sl = __builtin_ctzll(__ballot(above < q && notbelow >= q));
             const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)mg, sl);
@@ -299,83 +270,6 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
             }
         }
         CE_STAMP(blockIdx.x, 2)
-#if CE_SMALL_OWN_EXACT
-        // 3'. every thread evaluates the EXACT key of its own survivors (its
-        //     exact rows are in registers: no LDS row hand-off, every wave at
-        //     once) and appends the (~local slot, key) triples -- one slot per
-        //     pass (a lane with several survivors loops), one atomic per wave
-        //     and pass
-        {
-            uint32_t rem = 0;
-#pragma unroll
-            for (int v = 0; v < K; ++v) rem |= (sp[v] | (ak[v] >= thr)) ? (1u << v) : 0u;
-#pragma unroll 1
-            while (__ballot(rem != 0)) {  // wave-uniform
-                const bool has = rem != 0;
-                const int v = has ? __builtin_ctz(rem) : 0;
-                double x[C];
-#pragma unroll
-                for (int c = 0; c < C; ++c) x[c] = mrow[0][c];
-#pragma unroll
-                for (int vv = 1; vv < K; ++vv)
-#pragma unroll
-                    for (int c = 0; c < C; ++c) x[c] = v == vv ? mrow[vv][c] : x[c];
-                const uint64_t key = order_key(entropy_row<C>(x));
-                const uint64_t msk = __ballot(has);
-                int base = 0;
-                if (lane == 0) base = atomicAdd(&sm.cnt, (int)__popcll(msk));
-                base = __builtin_amdgcn_readfirstlane(base);
-                const int slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0));
-                CE_DASSERT(slot >= 0);
-                if (has && slot < SM::CAP)
-                    sm.cs[slot] = make_uint4(ntid - (uint32_t)(v * BS), (uint32_t)key, (uint32_t)(key >> 32), 0u);
-                rem &= rem - 1u;
-            }
-        }
-        __syncthreads();
-        CE_STAMP(blockIdx.x, 3)
-        const int nc = sm.cnt;
-        if (nc <= SM::CAP) {
-            CE_STAMP(blockIdx.x, 5)
-            auto rank_write = [&](int i) {  // survivor i takes the slot of its rank
-                const uint4 me = sm.cs[i];
-                int r = 0;
-                // 8 triples per LDS round trip; cs[nc, nc + 8) holds zero triples
-#pragma unroll 1
-                for (int j0 = 0; j0 < nc; j0 += 8) {
-                    CE_DASSERT(j0 + 8 <= SM::CAP + 8);
-                    uint4 a[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) a[k] = sm.cs[j0 + k];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) r = add_if_beats(r, me, a[k]);
-                }
-                CE_DASSERT(i < nc && r >= 0 && r < nc);
-                if (r < q) {
-                    ov[r] = key_to_val(((uint64_t)me.z << 32) | me.y);
-                    oi[r] = pos_of(~me.x);
-                }
-            };
-            if (tid < nc) rank_write(tid);
-            else if (tid < q) {  // fewer survivors than q: padding
-                ov[tid] = __longlong_as_double(0x7ff8000000000000ll);
-                oi[tid] = -1;
-            }
-            CE_STAMP(blockIdx.x, 4)
-        } else {
-            // overflow (> CAP items at or near the floor): per-wave lists + tree merge
-            RegTopQ tq;
-            tq.init(q);
-#pragma unroll
-            for (int v = 0; v < K; ++v) {
-                const bool ok = sp[v] | (ak[v] != 0);
-                const uint64_t key = ok ? order_key(entropy_row<C>(mrow[v])) : 0ull;
-                tq.offer(key, pos_of((uint32_t)(v * BS + tid)), ok);
-            }
-            block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
-        }
-#else
         // 3. survivors -> LDS rows: the wave's K ballots first, then ONE atomic
         //    per wave for all of its survivors
         {
@@ -491,7 +385,6 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LONG ? 4 : B
             }
             block_merge_write<W>(tq, sm.lists, q, nullptr, 0, ov, oi);
         }
-#endif
     }
 }
 

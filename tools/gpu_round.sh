@@ -166,7 +166,7 @@ scale)  # single-GPU proxies of one rank at 1/2/4/8 GPUs + the world-1 RCCL step
   step $? "scale proxy"
   ;;
 tests)  # selected GPU tests only: TESTS="file::name ..." or PYTEST_ARGS="-k expr" (failures keep going)
-  timeout -k 10 ${TLIM:-600} python -u -m pytest ${TESTS:-tests} -m gpu -v -s --timeout 400 --timeout-method thread ${TESTK:+-k "$TESTK"} ${PYTEST_ARGS} > "$OUT/pytest_sel.log" 2>&1
+  timeout -k 10 ${TLIM:-600} python -u -m pytest ${TESTS:-tests} -m gpu -v -s --timeout 400 --timeout-method thread ${TESTK:+-k "$TESTK"} ${PYTEST_ARGS} > "$OUT/pytest_sel${TAG}.log" 2>&1
   step $? "pytest selected"
   ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
