@@ -15,6 +15,7 @@
 #   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
+#   PHASE=gather     tools/gather_probe.py + FETCH / WRITE passes of the shuffled-frames kernel
 #   PHASE=scale      tools/scale_proxy.py (per-rank proxies; world-1 RCCL step eager vs HIP graph)
 #   PHASE=tests      selected GPU tests (TESTS=files, TESTK=-k expression, PYTEST_ARGS=...)
 # Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
@@ -169,10 +170,21 @@ tests)  # selected GPU tests only: TESTS="file::name ..." or PYTEST_ARGS="-k exp
   timeout -k 10 ${TLIM:-600} python -u -m pytest ${TESTS:-tests} -m gpu -v -s --timeout 400 --timeout-method thread ${TESTK:+-k "$TESTK"} ${PYTEST_ARGS} > "$OUT/pytest_sel${TAG}.log" 2>&1
   step $? "pytest selected"
   ;;
+gather)  # SURVEY §8(f)1 shuffled frames: the random-row probe + FETCH / WRITE passes of the fused shuffled kernel
+  timeout -k 10 300 python3 tools/gather_probe.py > "$OUT/gather_probe.json" 2> "$OUT/gather_probe.err"
+  step $? "gather probe"
+  cd /tmp
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/gather_fetch" -o run --output-format csv -- python3 "$ROOT/tools/gather_probe.py" --pmc > "$OUT/gather_fetch.log" 2>&1
+  step $? "gather fetch"
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof/gather_write" -o run --output-format csv -- python3 "$ROOT/tools/gather_probe.py" --pmc > "$OUT/gather_write.log" 2>&1
+  step $? "gather write"
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof/gather_trace" -o run --output-format csv -- python3 "$ROOT/tools/gather_probe.py" --pmc > "$OUT/gather_trace.log" 2>&1
+  step $? "gather trace"
+  ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale or tests" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather or tests" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
