@@ -16,6 +16,7 @@
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
 #   PHASE=gather     tools/gather_probe.py + FETCH / WRITE passes of the shuffled-frames kernel
+#   PHASE=framesab   tools/gather_probe.py per library build (LIBS="base x"), alternating
 #   PHASE=scale      tools/scale_proxy.py (per-rank proxies; world-1 RCCL step eager vs HIP graph)
 #   PHASE=tests      selected GPU tests (TESTS=files, TESTK=-k expression, PYTEST_ARGS=...)
 # Usage (from the repo root): gpurun -- 'PHASE=check bash tools/gpu_round.sh'
@@ -180,11 +181,24 @@ gather)  # SURVEY §8(f)1 shuffled frames: the random-row probe + FETCH / WRITE 
   step $? "gather write"
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof/gather_trace" -o run --output-format csv -- python3 "$ROOT/tools/gather_probe.py" --pmc > "$OUT/gather_trace.log" 2>&1
   step $? "gather trace"
+  timeout -k 10 120 "$ROOT/tools/_diag/random_row_probe" > "$OUT/random_rows.json" 2> "$OUT/random_rows.err"
+  step $? "random row probe"
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/rows32_fetch" -o run --output-format csv -- "$ROOT/tools/_diag/random_row_probe" 32 > "$OUT/rows32_fetch.log" 2>&1
+  step $? "random rows 32 fetch"
+  ;;
+framesab)  # the frames probe (tools/gather_probe.py) per library build (LIBS="base x"), alternating, 2 rounds
+  for rep in 1 2; do
+    for lib in ${LIBS:-base}; do
+      if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
+      CE_AMD_LIB=$L timeout -k 10 200 python3 tools/gather_probe.py > "$OUT/framesab_${lib}_$rep.json" 2> "$OUT/framesab_${lib}_$rep.err"
+      step $? "framesab $lib $rep"
+    done
+  done
   ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather or tests" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather, framesab or tests" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
