@@ -230,11 +230,28 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
         }
     RegTopQ tq;
     tq.init(q);
+    // the step's CSR offsets (this lane's song [f0, f1), the step's rows [R0,
+    // R1) of songs [t, t + G)) are loaded ONCE per step and one step ahead:
+    // the loads of step t + 1 are issued at the top of step t and land during
+    // its tiles, so no member's first tile waits on an offsets round trip
+    // (they were re-read per member before: 1M songs grouped 0.911 -> 0.880 ms,
+    // profiles/r05_frames_offsets_ab.json)
+    int64_t pf0 = 0, pf1 = 0, pR0 = 0, pR1 = 0;
+    auto load_offs = [&](int64_t t) {
+        const int64_t nn = t + sg;
+        const int64_t tg = t + G < hi ? t + G : hi;
+        pf0 = nn < hi ? a.off[nn] : 0;
+        pf1 = nn < hi ? a.off[nn + 1] : 0;
+        pR0 = a.off[t];
+        pR1 = a.off[tg];
+    };
+    if (lo < hi) load_offs(lo);
     for (int64_t t0 = lo; t0 < hi; t0 += step) {
         const int64_t n = t0 + sg;
         const bool live = n < hi;
-        const int64_t ng = t0 + G < hi ? t0 + G : hi;  // the step's songs [t0, ng)
         double acc = 0.0;  // np.add.reduce identity
+        const int64_t sf0 = pf0, sf1 = pf1, sR0 = pR0, sR1 = pR1;
+        if (t0 + step < hi) load_offs(t0 + step);
         if (!DMA && nf <= 4) {
             // direct loads (shuffled frames): each batch's 8 frame indices are
             // read ONCE for every frame-level member, then all members' rows of
@@ -242,7 +259,7 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
             // trips per batch instead of 2 per batch and member); each member
             // keeps its own sequential group sum, and the means meet in member
             // order below
-            const int64_t f0 = live ? a.off[n] : 0, f1 = live ? a.off[n + 1] : 0;
+            const int64_t f0 = sf0, f1 = sf1;
             CE_DASSERT(f0 >= 0 && f0 <= f1);
             constexpr int B = 8;  // (4: 1M songs equal, 1608 songs 38.6 -> 42.4 us)
             double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -303,13 +320,12 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                 const int64_t o = (live ? n : t0) * fm.ld + c;
                 mean = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o] : (double)static_cast<const float*>(fm.p)[o];
             } else {
-                const int64_t f0 = live ? a.off[n] : 0, f1 = live ? a.off[n + 1] : 0;
+                const int64_t f0 = sf0, f1 = sf1;
                 CE_DASSERT(f0 >= 0 && f0 <= f1);
                 double s = 0.0;
                 int cnt = 0;
                 const int RB = C * EB;
-                const int64_t R0 = a.off[t0];
-                const int64_t R1 = a.off[ng];
+                const int64_t R0 = sR0, R1 = sR1;
                 // the step's songs tile [R0, R1) (CSR offsets); a wave holding a song outside it
                 // (offsets not monotone) reads its rows directly instead
                 const bool inside = !live || (f0 >= R0 && f1 <= R1);
