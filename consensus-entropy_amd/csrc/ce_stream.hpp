@@ -171,7 +171,10 @@ __device__ __forceinline__ void wave_merge64(uint64_t& k, int64_t& i, uint64_t b
 // the last short slot issued with slot 0: C1 6.12 -> 6.42 us, C3 even; the
 // single-pool launches with 2 / all slots in flight: C1 5.86 -> 6.04 / 6.68 us,
 // the mix 6.6 -> 6.92 / 6.94 us.
-constexpr int kSmallThrottle = 1;
+#ifndef CE_SMALL_THR
+#define CE_SMALL_THR 1
+#endif
+constexpr int kSmallThrottle = CE_SMALL_THR;
 
 // no-op callback of CommitteeSrc::keys / rows_small (ce_kernels.hpp)
 struct NoHook {

@@ -8,7 +8,7 @@ permutation?  Times, on the configuration of tools/bench_configs.py --only 8
   fused          ops.select_frames(..., perm=perm) (k_frames_lanes, one pass)
   fused_grouped  the same frames already grouped (no perm, LDS-DMA tiles)
 and prints the useful bytes per second of each (rows read once + perm once).
-  python tools/gather_probe.py [--pmc]   (--pmc: only 5 fused shuffled calls, for a
+  python tools/gather_probe.py [--songs N] [--pmc]   (--pmc: only 5 fused shuffled calls, for a
                                           rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass)"""
 import json
 import os
@@ -37,7 +37,8 @@ def timed(fn, reps=20):
 
 def main():
     g = torch.Generator(device="cuda").manual_seed(1987)
-    songs, fps, C = 1_000_000, 40, 4
+    songs = int(sys.argv[sys.argv.index("--songs") + 1]) if "--songs" in sys.argv else 1_000_000
+    fps, C = 40, 4
     F = songs * fps
     fr = [torch.rand((F, C), dtype=torch.float64, device="cuda", generator=g) for _ in range(3)]
     cnn = torch.rand((songs, C), dtype=torch.float64, device="cuda", generator=g)
@@ -51,12 +52,13 @@ def main():
         print(json.dumps({"pmc_run": "fused shuffled x5", "useful_bytes_per_call": rows + F * 8 + songs * C * 8}))
         return
     out = {"config": f"{songs} songs x {fps} frames, 3 frame-level f64 members (C={C}, 32-B rows) + 1 song-level"}
-    t = timed(lambda: [torch.index_select(f, 0, perm) for f in fr])
+    reps = 200 if songs < 100_000 else 20
+    t = timed(lambda: [torch.index_select(f, 0, perm) for f in fr], reps)
     out["torch_gather"] = {"s": t, "useful_GB_per_s": (rows + 3 * F * 8) / t / 1e9,
                            "note": "perm read per member; the gathered copy is also written (not counted)"}
-    t = timed(lambda: ops.select_frames(fr + [cnn], offs, 10, perm=perm))
+    t = timed(lambda: ops.select_frames(fr + [cnn], offs, 10, perm=perm), reps)
     out["fused_shuffled"] = {"s": t, "useful_GB_per_s": (rows + F * 8 + songs * C * 8) / t / 1e9}
-    t = timed(lambda: ops.select_frames(fr + [cnn], offs, 10))
+    t = timed(lambda: ops.select_frames(fr + [cnn], offs, 10), reps)
     out["fused_grouped"] = {"s": t, "useful_GB_per_s": (rows + songs * C * 8) / t / 1e9}
     print(json.dumps(out, indent=1))
 

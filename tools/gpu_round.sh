@@ -190,7 +190,7 @@ framesab)  # the frames probe (tools/gather_probe.py) per library build (LIBS="b
   for rep in 1 2; do
     for lib in ${LIBS:-base}; do
       if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
-      CE_AMD_LIB=$L timeout -k 10 200 python3 tools/gather_probe.py > "$OUT/framesab_${lib}_$rep.json" 2> "$OUT/framesab_${lib}_$rep.err"
+      CE_AMD_LIB=$L timeout -k 10 200 python3 tools/gather_probe.py ${FRAMES_ARGS} > "$OUT/framesab${TAG}_${lib}_$rep.json" 2> "$OUT/framesab${TAG}_${lib}_$rep.err"
       step $? "framesab $lib $rep"
     done
   done
