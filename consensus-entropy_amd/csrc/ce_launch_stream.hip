@@ -21,6 +21,11 @@ static inline void with_batching(int M, F&& f) {
 static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                               const uint32_t* excl, const FoldOut* fold);
 
+#ifndef CE_WIDE_HEAVY_BLOCKS_PER_CU
+#define CE_WIDE_HEAVY_BLOCKS_PER_CU 2
+#endif
+constexpr int kWideHeavyBlocksPerCU = CE_WIDE_HEAVY_BLOCKS_PER_CU;
+
 bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                    const uint32_t* excl) {
     return launch_stream_impl(a, G, q, base_idx, w, st, excl, nullptr) != 0;
@@ -102,19 +107,17 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
         if constexpr (decltype(vec)::value) {
             constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
             // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
-#ifdef CE_WIDE_UNR_ROWS
-            constexpr int UNR = KCH >= CE_WIDE_UNR_ROWS ? 1 : CE_WIDE_UNR_ROWS / KCH;
-#else
             constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
-#endif
             // a 2-batch register ring (3 and 4 measured: 72.8 / 71.9 % vs 72.6 % at C5)
             auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
             note_kernel("ce::k_stream_wide2<%d, %d, %d>", DT, KCH, a.M % UNR == 0 ? UNR : 1);
-#ifdef CE_WIDE_BLOCKS_PER_CU
-            const int grid = std::min(resident_grid(kern, lds, G), CE_WIDE_BLOCKS_PER_CU * device_cus());
-#else
-            const int grid = resident_grid(kern, lds, G);
-#endif
+            // items of >= 16 KiB (the C5 config: 64 KB): 2 blocks (8 waves) per CU,
+            // not the 3 the occupancy allows -- fewer concurrent 64-KB item streams
+            // read HBM better (full C5 job on one box, 4 alternating reps: 0.820
+            // vs 0.803 of HBM and a third of the spread; 1 block per CU 0.741;
+            // profiles/r05_c5_grid_ab.json)
+            const int per_cu = R >= 16384 ? kWideHeavyBlocksPerCU : 1 << 20;
+            const int grid = std::min(resident_grid(kern, lds, G), per_cu * device_cus());
             stream_grid(sa, grid);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
         } else {  // strided / unaligned rows: the unpipelined wave-per-item kernel

@@ -130,8 +130,8 @@ c5)  # BASELINE configs[4]: rocprofv3 kernel trace of the full 50M x 32 x 1000 b
   timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE -d "$OUT/prof/c5_lds" -o run --output-format csv -- python3 "$ROOT/tools/bench_c5.py" $A > "$OUT/c5_lds.log" 2>&1
   step $? "c5 lds"
   ;;
-c5ab)  # A/B of library builds on the C5 job at 12M items (ABLIBS="base x ..."), builds alternating, 3 reps
-  for rep in 1 2 3; do
+c5ab)  # A/B of library builds on the C5 job at 12M items (ABLIBS="base x ...", ITEMS=, REPS=), builds alternating
+  for rep in $(seq 1 ${REPS:-3}); do
     for lib in ${ABLIBS:-base}; do
       if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
       CE_AMD_LIB=$L timeout -k 10 200 python3 tools/bench_c5.py --items ${ITEMS:-12000000} > "$OUT/c5ab_${lib}_$rep.json" 2> "$OUT/c5ab_${lib}_$rep.err"
