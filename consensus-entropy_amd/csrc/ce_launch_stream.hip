@@ -21,10 +21,9 @@ static inline void with_batching(int M, F&& f) {
 static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                               const uint32_t* excl, const FoldOut* fold);
 
-#ifndef CE_WIDE_HEAVY_BLOCKS_PER_CU
-#define CE_WIDE_HEAVY_BLOCKS_PER_CU 2
-#endif
-constexpr int kWideHeavyBlocksPerCU = CE_WIDE_HEAVY_BLOCKS_PER_CU;
+// items (M x C x size bytes) from which the wide stream runs one block per CU
+// with a deep register ring (below)
+constexpr int64_t kWideHeavyBytes = 16384;
 
 bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                    const uint32_t* excl) {
@@ -108,18 +107,40 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             constexpr int KCH = NPL / ChunkT<DT>::CPC > 0 ? NPL / ChunkT<DT>::CPC : 1;
             // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
             constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
-            // a 2-batch register ring (3 and 4 measured: 72.8 / 71.9 % vs 72.6 % at C5)
-            auto kern = (a.M % UNR == 0) ? k_stream_wide2<DT, KCH, UNR> : k_stream_wide2<DT, KCH, 1>;
-            note_kernel("ce::k_stream_wide2<%d, %d, %d>", DT, KCH, a.M % UNR == 0 ? UNR : 1);
-            // items of >= 16 KiB (the C5 config: 64 KB): 2 blocks (8 waves) per CU,
-            // not the 3 the occupancy allows -- fewer concurrent 64-KB item streams
-            // read HBM better (full C5 job on one box, 4 alternating reps: 0.820
-            // vs 0.803 of HBM and a third of the spread; 1 block per CU 0.741;
-            // profiles/r05_c5_grid_ab.json)
-            const int per_cu = R >= 16384 ? kWideHeavyBlocksPerCU : 1 << 20;
-            const int grid = std::min(resident_grid(kern, lds, G), per_cu * device_cus());
-            stream_grid(sa, grid);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
+            const int unr = a.M % UNR == 0 ? UNR : 1;
+            auto go = [&](auto kern, int nb, int per_cu) {
+                note_kernel("ce::k_stream_wide2<%d, %d, %d, %d>", DT, KCH, unr, nb);
+                const int grid = std::min(resident_grid(kern, lds, G), per_cu * device_cus());
+                stream_grid(sa, grid);
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
+            };
+            // A chunked job's chunks after the first (a running list seeds the
+            // prefilter's floor, so nearly every item skips its exact entropy)
+            // with heavy items (>= 16 KiB; the C5 config: 64 KB) run ONE block (4
+            // waves) per CU, each wave with an 8-batch register ring -- 7 batches
+            // (28 KB at C5) in flight.  Fewer concurrent item streams with more
+            // bytes each read HBM better: on the full C5 job 0.861 of HBM vs 0.833
+            // for the occupancy grid's 3 blocks with a 2-batch ring, and the spread
+            // 0.005 vs 0.044 (profiles/r05_c5_grid_ab.json: 2 blocks per CU 0.820,
+            // 1 block with a 2-batch ring 0.741, deeper rings at 2 per CU
+            // 0.813-0.817, a 12-batch ring spills).  Only 4 waves per CU cannot
+            // hide exact entropies, though: with every item exact (the build
+            // without the prefilter) the same grid reads 0.56 against 0.78, so the
+            // first chunk and single selections keep the occupancy grid.
+            bool heavy = false;
+            if constexpr (KCH <= 2)  // (wider lanes: 8 batches would spill)
+                heavy = R >= kWideHeavyBytes && fold != nullptr && fold->extra != nullptr && CE_WIDE_PREFILTER;
+            if (heavy) {
+                if constexpr (KCH <= 2) {
+                    if (unr == UNR) go(k_stream_wide2<DT, KCH, UNR, 8>, 8, 1);
+                    else go(k_stream_wide2<DT, KCH, 1, 8>, 8, 1);
+                }
+            } else {
+                // a 2-batch register ring at the occupancy grid (3 and 4 measured:
+                // 72.8 / 71.9 % vs 72.6 % at C5 in round 2)
+                if (unr == UNR) go(k_stream_wide2<DT, KCH, UNR, 2>, 2, 1 << 20);
+                else go(k_stream_wide2<DT, KCH, 1, 2>, 2, 1 << 20);
+            }
         } else {  // strided / unaligned rows: the unpipelined wave-per-item kernel
             if (sa.excl) {  // k_stream_wide takes no bitmap
                 rc_excl = CE_EUNSUPPORTED;
