@@ -367,11 +367,15 @@ struct WaveListsT {
 };
 using WaveLists = WaveListsT<4>;
 
-template <int S>
+template <int S, int RING = 1>
 struct StreamSmemNMC {
-    char tile[4][64 * 16 * S];  // one staging tile per wave
+    char tile[4][RING][64 * 16 * S];  // RING staging tiles per wave
     WaveLists lists;
 };
+
+#ifndef CE_NMC_RING
+#define CE_NMC_RING 1
+#endif
 
 struct StreamArgs {
     const void* p;
@@ -764,7 +768,8 @@ template <int DT, int C, int S, int AUX, bool MNC = false>
 __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* __restrict__ wc) {
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     CE_DASSERT((int)gridDim.x <= a.nlists && q >= 1 && q <= kStreamMaxQ);
-    __shared__ __attribute__((aligned(16))) StreamSmemNMC<S> sm;
+    constexpr int RING = (CE_NMC_RING == 2 && S <= 16) ? 2 : 1;  // two 16-KiB tiles per wave fit one block per CU
+    __shared__ __attribute__((aligned(16))) StreamSmemNMC<S, RING> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int64_t lo, hi, step;
     // tile distribution (measured on two boxes, alternating runs,
@@ -789,23 +794,35 @@ __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* _
     RegTopQ tq;
     tq.init(q);
     const char* base = static_cast<const char*>(a.p);
-    char* lds = sm.tile[w];
     constexpr int EB = DT == kF64 ? 8 : (DT == kF32 ? 4 : 2);
     const int64_t sMb = a.sM * EB;
-    auto issue = [&](int64_t t, int nv) {
+    auto issue = [&](int64_t t, int nv, int slot) {
+        char* lds = sm.tile[w][slot];
         if constexpr (MNC) ItemTile<S>::template issue_mnc<AUX>(base, t, nv, sMb, lds);
         else ItemTile<S>::template issue<AUX>(base, t, nv, lds);
     };
     ItemTile<S> t;
-    if (lo < hi) issue(lo, (int)min<int64_t>(64, hi - lo));
+#pragma unroll
+    for (int r = 0; r < RING; ++r)
+        if (lo + r * step < hi) issue(lo + r * step, (int)min<int64_t>(64, hi - lo - r * step), r);
+    int slot = 0;
     for (int64_t t0 = lo; t0 < hi; t0 += step) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // S DMA instructions per tile (always: short tiles re-read their last row),
+        // so the tiles issued after this one are (RING - 1) * S instructions
+        if constexpr (RING == 2) {
+            if (t0 + step < hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const char* lds = sm.tile[w][slot];
         if constexpr (MNC) t.read_mnc(lds);
         else t.read(lds);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        const int64_t t1 = t0 + step;
-        if (t1 < hi) issue(t1, (int)min<int64_t>(64, hi - t1));
+        const int64_t t1 = t0 + RING * step;
+        if (t1 < hi) issue(t1, (int)min<int64_t>(64, hi - t1), slot);
+        slot = RING == 1 ? 0 : slot ^ 1;
         double mean[C];
         t.template mean<DT, C>(a.dM, a.invM, a.pow2, mean);
         const double h = entropy_row<C>(mean);
