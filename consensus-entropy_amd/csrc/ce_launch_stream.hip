@@ -55,9 +55,10 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     if (dense_nmc && (R == 256 || R == 512)) {
 #define CE_S(DT_, C_, S_)                                                                                   \
     if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
-        auto kern = k_stream_nmc<DT_, C_, S_, 2>;                                                         \
+        constexpr int RING_ = S_ == 16 ? 2 : 1; /* two 16-KiB tiles per wave: one block per CU */          \
+        auto kern = k_stream_nmc<DT_, C_, S_, 2, false, RING_>;                                           \
         const int grid = resident_grid(kern, 0, G);                                                       \
-        note_kernel("ce::k_stream_nmc<%d, %d, %d, 2, false>", DT_, C_, S_);                                \
+        note_kernel("ce::k_stream_nmc<%d, %d, %d, 2, false, %d>", DT_, C_, S_, RING_);                     \
         stream_grid(sa, grid);                                                                            \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                               \
         return folded;                                                                                    \
@@ -73,9 +74,10 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
     if (dense_mnc) {
 #define CE_SM(DT_, C_, M_)                                                                              \
     if (a.dt == DT_ && a.C == C_ && a.M == M_) {                                                       \
-        auto kern = k_stream_nmc<DT_, C_, M_, 2, true>;                                                \
+        constexpr int RING_ = M_ == 16 ? 2 : 1; /* as measured: 16 members (16-KiB tiles) */          \
+        auto kern = k_stream_nmc<DT_, C_, M_, 2, true, RING_>;                                         \
         const int grid = resident_grid(kern, 0, G);                                                    \
-        note_kernel("ce::k_stream_nmc<%d, %d, %d, 2, true>", DT_, C_, M_);                              \
+        note_kernel("ce::k_stream_nmc<%d, %d, %d, 2, true, %d>", DT_, C_, M_, RING_);                   \
         stream_grid(sa, grid);                                                                         \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                            \
         return folded;                                                                                 \

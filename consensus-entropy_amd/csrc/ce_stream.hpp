@@ -373,9 +373,7 @@ struct StreamSmemNMC {
     WaveLists lists;
 };
 
-#ifndef CE_NMC_RING
-#define CE_NMC_RING 1
-#endif
+
 
 struct StreamArgs {
     const void* p;
@@ -764,11 +762,17 @@ __device__ inline void fold_merge(uint32_t* ctr, double* oval, int64_t* oidx, Ca
 // Item-major, dense rows of 16*S bytes, LDS-DMA staged (AUX: DMA cache policy);
 // MNC: the member-major stack with 16-B member rows instead (S = M members,
 // member stride a.sM elements).
-template <int DT, int C, int S, int AUX, bool MNC = false>
+// RING tiles per wave: 2 (the default for 16-KiB tiles) puts the next two
+// tiles in flight while one is read -- 139 KB of LDS, so ONE block (4 waves)
+// per CU instead of 2 blocks with one tile each: the same bytes in flight from
+// half as many streams.  Measured on one box, alternating (profiles/
+// r05_nmc_ring_ab.json): [N,M,C] 0.856-0.860 -> 0.883-0.884 of HBM, [M,N,C]
+// 0.835 -> 0.846.
+template <int DT, int C, int S, int AUX, bool MNC = false, int RING = 1>
 __global__ __launch_bounds__(256) void k_stream_nmc(StreamArgs a, int q, Cand* __restrict__ wc) {
+    static_assert(RING == 1 || RING == 2, "one or two tiles per wave");
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     CE_DASSERT((int)gridDim.x <= a.nlists && q >= 1 && q <= kStreamMaxQ);
-    constexpr int RING = (CE_NMC_RING == 2 && S <= 16) ? 2 : 1;  // two 16-KiB tiles per wave fit one block per CU
     __shared__ __attribute__((aligned(16))) StreamSmemNMC<S, RING> sm;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int64_t lo, hi, step;

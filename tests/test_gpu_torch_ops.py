@@ -170,10 +170,10 @@ def test_last_kernel_names_the_stage1_kernel(tops):
     lib = ce_amd._lib.load()
     P = pool(41, (200_000, 16, 4))
     ops.select_mc(P, 10, "NMC")
-    assert lib.ce_last_kernel().decode() == "ce::k_stream_nmc<0, 4, 16, 2, false>"
+    assert lib.ce_last_kernel().decode() == "ce::k_stream_nmc<0, 4, 16, 2, false, 2>"
     Pm = P.permute(1, 0, 2).contiguous()
     ops.select_mc(Pm, 10, "MNC")
-    assert lib.ce_last_kernel().decode() == "ce::k_stream_nmc<0, 4, 16, 2, true>"
+    assert lib.ce_last_kernel().decode() == "ce::k_stream_nmc<0, 4, 16, 2, true, 2>"
     small = pool(42, (4, 1608, 4))
     ops.select_mc(small, 10, "MNC")
     assert lib.ce_last_kernel().decode().startswith("ce::k_select_tiles<ce::CommitteeSrc<0, 4, true>")
