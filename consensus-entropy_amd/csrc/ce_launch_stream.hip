@@ -21,6 +21,11 @@ static inline void with_batching(int M, F&& f) {
 static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                               const uint32_t* excl, const FoldOut* fold);
 
+// the LDS-DMA loads' cache-policy bits (2: non-temporal -- the pool is read once)
+#ifndef CE_NMC_AUX
+#define CE_NMC_AUX 2
+#endif
+
 // items (M x C x size bytes) from which the wide stream runs one block per CU
 // with a deep register ring (below)
 constexpr int64_t kWideHeavyBytes = 16384;
@@ -56,9 +61,9 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
 #define CE_S(DT_, C_, S_)                                                                                   \
     if (a.dt == DT_ && a.C == C_ && R == 16 * S_) {                                                       \
         constexpr int RING_ = S_ == 16 ? 2 : 1; /* two 16-KiB tiles per wave: one block per CU */          \
-        auto kern = k_stream_nmc<DT_, C_, S_, 2, false, RING_>;                                           \
+        auto kern = k_stream_nmc<DT_, C_, S_, CE_NMC_AUX, false, RING_>;                                  \
         const int grid = resident_grid(kern, 0, G);                                                       \
-        note_kernel("ce::k_stream_nmc<%d, %d, %d, 2, false, %d>", DT_, C_, S_, RING_);                     \
+        note_kernel("ce::k_stream_nmc<%d, %d, %d, %d, false, %d>", DT_, C_, S_, CE_NMC_AUX, RING_);        \
         stream_grid(sa, grid);                                                                            \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, sa, q, w.c);                               \
         return folded;                                                                                    \
