@@ -242,6 +242,19 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // Loads of one member's C class probabilities of one item, widened to f64.
 // VEC: C contiguous and 16-B (f32/f64) / 8-B (bf16) aligned -> vector loads.
 // ---------------------------------------------------------------------------
+// the member loads' cache policy: non-temporal (1, default) or plain (0; A/B builds)
+#ifndef CE_MEMBER_NT
+#define CE_MEMBER_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T member_ld(const T* p) {
+#if CE_MEMBER_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 template <int DT, int C, bool VEC>
 struct MemberLoad;
 
@@ -252,7 +265,7 @@ struct MemberLoad<kF32, C, true> {
     __device__ __forceinline__ void load(const void* base, int64_t off, int64_t) {
         const f32x4* p = reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + off);
 #pragma unroll
-        for (int k = 0; k < C / 4; ++k) v[k] = __builtin_nontemporal_load(p + k);
+        for (int k = 0; k < C / 4; ++k) v[k] = member_ld(p + k);
     }
     __device__ __forceinline__ void pin() const {
 #pragma unroll
@@ -285,7 +298,7 @@ struct MemberLoad<kF64, C, true> {
     __device__ __forceinline__ void load(const void* base, int64_t off, int64_t) {
         const f64x2* p = reinterpret_cast<const f64x2*>(static_cast<const double*>(base) + off);
 #pragma unroll
-        for (int k = 0; k < C / 2; ++k) v[k] = __builtin_nontemporal_load(p + k);
+        for (int k = 0; k < C / 2; ++k) v[k] = member_ld(p + k);
     }
     __device__ __forceinline__ void pin() const {
 #pragma unroll
@@ -314,7 +327,7 @@ struct MemberLoad<kBF16, C, true> {
     __device__ __forceinline__ void load(const void* base, int64_t off, int64_t) {
         const u32x2* p = reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(base) + off);
 #pragma unroll
-        for (int k = 0; k < C / 4; ++k) v[k] = __builtin_nontemporal_load(p + k);
+        for (int k = 0; k < C / 4; ++k) v[k] = member_ld(p + k);
     }
     __device__ __forceinline__ void pin() const {
 #pragma unroll
