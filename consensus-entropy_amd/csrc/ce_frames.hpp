@@ -187,6 +187,13 @@ __global__ __launch_bounds__(256) void k_frames_entropy(FrameArgs a, double* __r
     }
 }
 
+// the shuffled gather's row loads non-temporal: each random 32-B row is read
+// once (1M songs x 40 frames, 3 members: 2.495 -> 2.284 ms on one box,
+// profiles/r05_frames_gather_nt.json)
+#ifndef CE_FRAMES_GATHER_NT
+#define CE_FRAMES_GATHER_NT 1
+#endif
+
 // The same selection with C lanes per song (lane = (song, class), 64 / C songs
 // per wave step): each lane keeps ONE class's sequential group sum, so the
 // frame rows of the wave's songs are read as whole rows.  Grouped frames (no
@@ -279,8 +286,13 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
 #pragma unroll
                         for (int u = 0; u < B; ++u) {
                             const int64_t o = r[u] * fm.ld + c;
+#if CE_FRAMES_GATHER_NT
+                            v[k][u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
+                                                    : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
+#else
                             v[k][u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
                                                     : (double)static_cast<const float*>(fm.p)[o];
+#endif
                         }
                     }
                 }
@@ -380,8 +392,13 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                             const int64_t f = fb + u < f1 ? fb + u : f1 - 1;
                             const int64_t r = a.perm ? a.perm[f] : f;
                             const int64_t o = r * fm.ld + c;
+#if CE_FRAMES_GATHER_NT
+                            v[u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
+                                                 : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
+#else
                             v[u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
                                                  : (double)static_cast<const float*>(fm.p)[o];
+#endif
                         }
 #pragma unroll
                         for (int u = 0; u < B; ++u)

@@ -12,7 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
-template <int S>
+template <int S, bool NT>
 __global__ __launch_bounds__(256) void k_rows(const double* __restrict__ buf, int64_t log2_rows, int64_t n_reads,
                                               double* __restrict__ sink) {
     constexpr int L = S / 8;  // lanes per row
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void k_rows(const double* __restrict__ buf, in
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const uint64_t r = ((uint64_t)(i + u * groups) * 0x9E3779B97F4A7C15ull) & mask;  // odd multiplier: bijective mod 2^k
-            v[u] = buf[r * L + sub];
+            v[u] = NT ? __builtin_nontemporal_load(buf + r * L + sub) : buf[r * L + sub];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += v[u];
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void k_rows(const double* __restrict__ buf, in
     if (acc == 1.2345) sink[0] = acc;
 }
 
-template <int S>
+template <int S, bool NT = false>
 static void run(const double* buf, int64_t bytes, double* sink) {
     int64_t log2_rows = 0;
     while (((int64_t)S << (log2_rows + 1)) <= bytes) ++log2_rows;
@@ -43,19 +43,19 @@ static void run(const double* buf, int64_t bytes, double* sink) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    hipLaunchKernelGGL(k_rows<S>, dim3(grid), dim3(256), 0, 0, buf, log2_rows, n_reads, sink);  // warm-up
+    hipLaunchKernelGGL((k_rows<S, NT>), dim3(grid), dim3(256), 0, 0, buf, log2_rows, n_reads, sink);  // warm-up
     float best = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
         hipEventRecord(a);
-        hipLaunchKernelGGL(k_rows<S>, dim3(grid), dim3(256), 0, 0, buf, log2_rows, n_reads, sink);
+        hipLaunchKernelGGL((k_rows<S, NT>), dim3(grid), dim3(256), 0, 0, buf, log2_rows, n_reads, sink);
         hipEventRecord(b);
         hipEventSynchronize(b);
         float ms = 0;
         hipEventElapsedTime(&ms, a, b);
         best = ms < best ? ms : best;
     }
-    printf("{\"row_bytes\": %d, \"rows\": %lld, \"ms\": %.3f, \"G_rows_per_s\": %.2f, \"useful_GB_per_s\": %.1f}\n", S,
-           (long long)n_reads, best, n_reads / (best * 1e-3) / 1e9, n_reads * (double)S / (best * 1e-3) / 1e9);
+    printf("{\"row_bytes\": %d, \"nontemporal\": %s, \"rows\": %lld, \"ms\": %.3f, \"G_rows_per_s\": %.2f, \"useful_GB_per_s\": %.1f}\n", S,
+           NT ? "true" : "false", (long long)n_reads, best, n_reads / (best * 1e-3) / 1e9, n_reads * (double)S / (best * 1e-3) / 1e9);
     hipEventDestroy(a);
     hipEventDestroy(b);
 }
@@ -77,6 +77,10 @@ int main(int argc, char** argv) {
     if (!only || only == 64) run<64>(buf, bytes, sink);
     if (!only || only == 128) run<128>(buf, bytes, sink);
     if (!only || only == 256) run<256>(buf, bytes, sink);
+    // non-temporal loads (each random row is read once)
+    if (!only || only == 8) run<8, true>(buf, bytes, sink);
+    if (!only || only == 32) run<32, true>(buf, bytes, sink);
+    if (!only || only == 128) run<128, true>(buf, bytes, sink);
     hipFree(buf);
     hipFree(sink);
     return 0;
