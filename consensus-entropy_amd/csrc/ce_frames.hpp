@@ -189,7 +189,9 @@ __global__ __launch_bounds__(256) void k_frames_entropy(FrameArgs a, double* __r
 
 // the shuffled gather's row loads non-temporal: each random 32-B row is read
 // once (1M songs x 40 frames, 3 members: 2.495 -> 2.284 ms on one box,
-// profiles/r05_frames_gather_nt.json)
+// profiles/r05_frames_random_rows.json).  Grouped rows (no perm) keep plain
+// loads: neighbouring lanes share their lines (the segment mean with nt loads:
+// 374 -> 673 us grouped, profiles/r05_segment_nt_ab.json)
 #ifndef CE_FRAMES_GATHER_NT
 #define CE_FRAMES_GATHER_NT 1
 #endif
@@ -287,8 +289,12 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                         for (int u = 0; u < B; ++u) {
                             const int64_t o = r[u] * fm.ld + c;
 #if CE_FRAMES_GATHER_NT
-                            v[k][u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
-                                                    : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
+                            if (a.perm)  // wave-uniform: shuffled rows are read once; grouped rows share lines
+                                v[k][u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
+                                                        : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
+                            else
+                                v[k][u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
+                                                        : (double)static_cast<const float*>(fm.p)[o];
 #else
                             v[k][u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
                                                     : (double)static_cast<const float*>(fm.p)[o];
@@ -393,8 +399,12 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                             const int64_t r = a.perm ? a.perm[f] : f;
                             const int64_t o = r * fm.ld + c;
 #if CE_FRAMES_GATHER_NT
-                            v[u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
-                                                 : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
+                            if (a.perm)  // wave-uniform, as above
+                                v[u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
+                                                     : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
+                            else
+                                v[u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
+                                                     : (double)static_cast<const float*>(fm.p)[o];
 #else
                             v[u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
                                                  : (double)static_cast<const float*>(fm.p)[o];
