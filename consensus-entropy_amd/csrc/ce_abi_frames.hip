@@ -1,6 +1,7 @@
 // ce_abi_frames.hip -- C-ABI (include/ce.h): frames -> committee entropy ->
 // top-q in one pass (k_frames_select, ce_frames.hpp).
 #include "ce_frames.hpp"
+#include "ce_abi.hpp"
 #include "ce_host.hpp"
 
 using namespace ce;
@@ -44,6 +45,7 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     fa.base_idx = base_idx;
     fa.nlists = G;
     hipStream_t st = (hipStream_t)stream;
+    note_kernel("%s", "");
     if (q == 0) return CE_OK;
     if (q > kStreamMaxQ) {  // per-song entropies to HBM, then the lists (q <= CE_MAX_Q) or the sort path
         double* ent;
@@ -96,18 +98,22 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     // LDS-DMA tiles for grouped frames once every wave runs >= 4 steps: at the
     // reference's 1608 songs x 40 frames the tile round trips are exposed
     // (DMA 44.6 us, direct 31.7 us); at 1M songs the tiles win (0.92 vs 1.49 ms)
-    auto lanes_go = [&](auto dma_kern, auto direct_kern, int step) {
+    // (large shuffled pools: the gather's row loads non-temporal, k_frames_lanes GNT)
+    auto lanes_go = [&](auto dma_kern, auto direct_kern, auto gather_kern, int step) {
         const int grid = resident_grid(dma_kern, 0, G);
         const int64_t steps_per_wave = cdiv(cdiv(N, (int64_t)grid * 4), (int64_t)step);
         const bool dma = !perm_or_null && (dma_env >= 0 ? dma_env == 1 : steps_per_wave >= 4);
+        const bool gnt = !dma && perm_or_null && steps_per_wave >= 4;
+        note_kernel("ce::k_frames_lanes<%d, %s, %s>", 64 / step, dma ? "true" : "false", gnt ? "true" : "false");
         if (dma) go(dma_kern, step);
+        else if (gnt) go(gather_kern, step);
         else go(direct_kern, step);
     };
     switch (C) {
-        case 2: lanes_go(k_frames_lanes<2, true>, k_frames_lanes<2, false>, 32); break;
-        case 3: go(k_frames_select<3>, 64); break;
-        case 4: lanes_go(k_frames_lanes<4, true>, k_frames_lanes<4, false>, 16); break;
-        default: lanes_go(k_frames_lanes<8, true>, k_frames_lanes<8, false>, 8); break;
+        case 2: lanes_go(k_frames_lanes<2, true>, k_frames_lanes<2, false>, k_frames_lanes<2, false, true>, 32); break;
+        case 3: note_kernel("%s", "ce::k_frames_select<3>"); go(k_frames_select<3>, 64); break;
+        case 4: lanes_go(k_frames_lanes<4, true>, k_frames_lanes<4, false>, k_frames_lanes<4, false, true>, 16); break;
+        default: lanes_go(k_frames_lanes<8, true>, k_frames_lanes<8, false>, k_frames_lanes<8, false, true>, 8); break;
     }
     return check_launch("ce_select_frames");
 }

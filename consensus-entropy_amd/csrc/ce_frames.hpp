@@ -187,15 +187,6 @@ __global__ __launch_bounds__(256) void k_frames_entropy(FrameArgs a, double* __r
     }
 }
 
-// the shuffled gather's row loads non-temporal: each random 32-B row is read
-// once (1M songs x 40 frames, 3 members: 2.495 -> 2.284 ms on one box,
-// profiles/r05_frames_random_rows.json).  Grouped rows (no perm) keep plain
-// loads: neighbouring lanes share their lines (the segment mean with nt loads:
-// 374 -> 673 us grouped, profiles/r05_segment_nt_ab.json)
-#ifndef CE_FRAMES_GATHER_NT
-#define CE_FRAMES_GATHER_NT 1
-#endif
-
 // The same selection with C lanes per song (lane = (song, class), 64 / C songs
 // per wave step): each lane keeps ONE class's sequential group sum, so the
 // frame rows of the wave's songs are read as whole rows.  Grouped frames (no
@@ -211,8 +202,14 @@ __global__ __launch_bounds__(256) void k_frames_entropy(FrameArgs a, double* __r
 // meet by lane shuffles; every lane of the song computes its entropy (the
 // group's lane 0 offers it).  Same values as k_frames_select.
 // DMA = false: direct loads only, no LDS tiles -- the 64 KiB of tiles would
-// cap the gather (shuffled frames) at 2 blocks per CU.
-template <int C, bool DMA>
+// cap the gather (shuffled frames) at 2 blocks per CU.  GNT: the direct row
+// loads non-temporal -- for large shuffled pools, whose random rows are each
+// read once (1M songs x 40 frames: 2.49 -> 2.30 ms); at the reference's 1608
+// songs it costs 3 us (39.7 -> 42.2), and grouped rows share their lines (the
+// segment mean with nt loads: 374 -> 673 us), so the host picks it only for
+// shuffled pools of >= 4 steps per wave (profiles/r05_frames_random_rows.json,
+// r05_segment_nt_ab.json).
+template <int C, bool DMA, bool GNT = false>
 __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* __restrict__ wc) {
     static_assert(64 % C == 0, "C divides the wave");
     constexpr int G = 64 / C;  // songs per wave step
@@ -288,17 +285,12 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
 #pragma unroll
                         for (int u = 0; u < B; ++u) {
                             const int64_t o = r[u] * fm.ld + c;
-#if CE_FRAMES_GATHER_NT
-                            if (a.perm)  // wave-uniform: shuffled rows are read once; grouped rows share lines
+                            if constexpr (GNT)  // shuffled rows of a large pool: each read once
                                 v[k][u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
                                                         : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
                             else
                                 v[k][u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
                                                         : (double)static_cast<const float*>(fm.p)[o];
-#else
-                            v[k][u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
-                                                    : (double)static_cast<const float*>(fm.p)[o];
-#endif
                         }
                     }
                 }
@@ -398,17 +390,12 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                             const int64_t f = fb + u < f1 ? fb + u : f1 - 1;
                             const int64_t r = a.perm ? a.perm[f] : f;
                             const int64_t o = r * fm.ld + c;
-#if CE_FRAMES_GATHER_NT
-                            if (a.perm)  // wave-uniform, as above
+                            if constexpr (GNT)
                                 v[u] = fm.dt == kF64 ? __builtin_nontemporal_load(static_cast<const double*>(fm.p) + o)
                                                      : (double)__builtin_nontemporal_load(static_cast<const float*>(fm.p) + o);
                             else
                                 v[u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
                                                      : (double)static_cast<const float*>(fm.p)[o];
-#else
-                            v[u] = fm.dt == kF64 ? static_cast<const double*>(fm.p)[o]
-                                                 : (double)static_cast<const float*>(fm.p)[o];
-#endif
                         }
 #pragma unroll
                         for (int u = 0; u < B; ++u)

@@ -795,6 +795,36 @@ def test_frames_fused_selection(ce, grouped):
     assert np.array_equal(idx_np(ce.ops.select_mc(stack, 10, "MNC")[1]), O.oracle_select_mc(P, 10, "MNC")[1])
 
 
+@pytest.mark.parametrize("C", [4, 8, 2])
+def test_frames_large_shuffled_gather(ce, C):
+    """A shuffled frame pool large enough (>= 4 steps per wave) for the
+    non-temporal gather (k_frames_lanes<C, false, true>, ce_abi_frames.hip):
+    300k songs of 1..7 frames, an f64 and an f32 frame member plus a song-level
+    member, against the restated groupby mean + oracle; the reference-sized
+    pool keeps the plain gather."""
+    from oracle import ce_oracle as O
+    from oracle.ce_oracle import ref_group_mean
+
+    lib = ce._lib.load()
+    rng = np.random.default_rng(300 + C)
+    S = 300_000
+    s_id = rng.permutation(np.repeat(np.arange(S) * 5 + 2, rng.integers(1, 8, S)))
+    F = len(s_id)
+    frame_members = []
+    for dt in (np.float64, np.float32):
+        e = -np.log(rng.random((F, C)))
+        frame_members.append((e / e.sum(-1, keepdims=True)).astype(dt))
+    song = rng.random((S, C)).astype(np.float32)
+    P = np.array([ref_group_mean(m, s_id)[0] for m in frame_members] + [song])
+    for q in (1, 10, 64):
+        got, _ = ce.select_from_frames(frame_members + [song], s_id, q)
+        assert lib.ce_last_kernel().decode() == f"ce::k_frames_lanes<{C}, false, true>"
+        assert np.array_equal(got, O.oracle_select_mc(P, q, "MNC")[1]), q
+    small = rng.permutation(np.repeat(np.arange(1608) * 5 + 2, 40))
+    ce.select_from_frames([np.full((len(small), C), 1.0 / C)], small, 10)
+    assert lib.ce_last_kernel().decode() == f"ce::k_frames_lanes<{C}, false, false>"
+
+
 def _shrinking_reference(mode, epochs, q, committees, hc):
     """The reference's epoch loop on the host: pools shrink by the picks
     (amg_test.py:455, :484, :521-531) and every epoch selects on what is left
