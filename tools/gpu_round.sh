@@ -195,10 +195,19 @@ framesab)  # the frames probe (tools/gather_probe.py) per library build (LIBS="b
     done
   done
   ;;
+memab)  # member-inference configs (bench_configs.py --only 6: GNB, SGD) per library build (LIBS="base x"), alternating, 2 rounds
+  for rep in 1 2; do
+    for lib in ${LIBS:-base}; do
+      if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
+      CE_AMD_LIB=$L timeout -k 10 200 python3 tools/bench_configs.py --only 6 > "$OUT/memab_${lib}_$rep.log" 2>&1
+      step $? "memab $lib $rep"
+    done
+  done
+  ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather, framesab or tests" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather, framesab, memab or tests" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
