@@ -17,7 +17,20 @@ every rank's q candidate records (16 B each) + the merge
 Dirichlet(1) member rows (1% un-normalised, like sigmoid CNN members), seed
 1987, generated on the device before timing.
 
+Ranks: under torchrun (WORLD_SIZE set) this process is one rank.  A plain
+`python3 bench.py --gpus N` (N > 1) starts the N ranks itself -- N fresh child
+processes with torchrun's environment, started before the parent makes any GPU
+call -- and exits with the worst rank's status; rank 0's line is the output.
+A --gpus that disagrees with WORLD_SIZE, or more ranks than visible GPUs
+(outside a CE_AMD_REHEARSAL=1 rehearsal), exits 2 without a line.
+
 Also reported:
+  ranks / backend  the process group's size and backend (None at N=1)
+  selected_equal_n1  the merged selection equals the N=1 selection of the same
+                pool: rank 0 re-selects the whole pool after the timed region
+                on its GPU by the chunked single-GPU path (ops.MCChunkJob), and
+                compares with the committed 1-GPU record (profiles/
+                selected_n1.json) when there is one; a mismatch exits 3
   roofline      the selection kernel (stage 1 + folded stage 2): algorithmic
                 bytes (N_local x 256 B) / its mean duration from HIP events on
                 the launch stream, vs 8 TB/s;
@@ -156,7 +169,7 @@ def cpu_baseline(n_items, M, C, q, seed=1987):
         "value": n_items / t,
         "unit": "items/s",
         "cores": 1,
-        "kind": "port",
+        "kind": "reference",
         "multicore": multicore,
         "sample": (f"reference expressions amg_test.py:441-445 verbatim (np.mean(np.array(pred_prob),0), "
                    f"scipy.stats.entropy(axis=1), np.argsort()[::-1][:{q}]) on {n_items} items x {M} mixed "
@@ -242,6 +255,129 @@ def host_cpu_share():
             "rule": "GPU pool: 16 host CPUs per GPU job"}
 
 
+class LaunchError(SystemExit):
+    """A --gpus request bench.py must refuse (exit status 2, no JSON line)."""
+
+    def __init__(self, msg):
+        log(f"bench.py: {msg}")
+        super().__init__(2)
+
+
+def launch_plan(gpus, env, visible):
+    """What bench.py does for `--gpus gpus` given the environment and the
+    number of visible GPUs (torch.cuda.device_count(), which does not
+    initialise the GPU on this image):
+      ("run", world)   run this process as one rank of `world` (torchrun, or
+                       the launcher's child, set WORLD_SIZE), or alone at N=1
+      ("spawn", n)     start n ranks as child processes and wait for them
+    Refuses (LaunchError): --gpus < 1, a --gpus that disagrees with an
+    explicit WORLD_SIZE, or more ranks than visible GPUs outside a one-GPU
+    rehearsal (CE_AMD_REHEARSAL=1) -- never a 1-GPU line for --gpus N."""
+    if gpus < 1:
+        raise LaunchError(f"--gpus {gpus} must be >= 1")
+    rehearsal = env.get("CE_AMD_REHEARSAL") == "1"
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise LaunchError(f"WORLD_SIZE={world} disagrees with --gpus {gpus}")
+        if not rehearsal and world > 1 and world > visible:
+            raise LaunchError(f"{world} ranks but {visible} visible GPU(s)")
+        return ("run", world)
+    if not rehearsal and gpus > 1 and gpus > visible:
+        raise LaunchError(f"--gpus {gpus} but {visible} visible GPU(s) (CE_AMD_REHEARSAL=1 shares them over gloo)")
+    return ("run", 1) if gpus == 1 else ("spawn", gpus)
+
+
+def free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(env, rank, world, port):
+    """The environment of child rank `rank` (what torchrun would set)."""
+    out = dict(env)
+    out.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    out.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL needs dmabuf IPC on this pool
+    return out
+
+
+def spawn_ranks(cmd, n, env=None, poll_s=0.2):
+    """Run `cmd` as n ranks (fresh child processes, each with its rank's
+    environment; the parent never touches the GPU) and return the worst exit
+    status: the first failing rank's, 128 + signal for a killed one.  When one
+    rank fails, the others get SIGTERM after a grace period (the fail-fast
+    collective timeout would end them anyway).  Rank 0's stdout is the
+    parent's stdout: the JSON line."""
+    import signal
+    import subprocess
+
+    env = dict(os.environ if env is None else env)
+    port = free_port()
+    procs = [subprocess.Popen(cmd, env=rank_env(env, r, n, port)) for r in range(n)]
+    rcs = [None] * n
+    failed_at = None
+    try:
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None and p.poll() is not None:
+                    rcs[r] = p.returncode
+                    if p.returncode != 0 and failed_at is None:
+                        failed_at = time.monotonic()
+            if failed_at is not None and time.monotonic() - failed_at > 30:
+                for r, p in enumerate(procs):
+                    if rcs[r] is None:
+                        p.send_signal(signal.SIGTERM)
+                failed_at = float("inf")
+            time.sleep(poll_s)
+    finally:
+        for r, p in enumerate(procs):
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    worst = 0
+    for rc in rcs:
+        rc = 128 - rc if rc is not None and rc < 0 else rc
+        if rc and not worst:
+            worst = rc
+    return worst
+
+
+SELECTED_FILE = os.path.join(ROOT, "profiles", "selected_n1.json")
+
+
+def recorded_selection(key):
+    """The committed N=1 selection of a workload (profiles/selected_n1.json:
+    the driver's own 1-GPU line), or None."""
+    try:
+        with open(SELECTED_FILE) as f:
+            return json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def n1_selection(N, M, C, q, layout, device):
+    """The N=1 selection of the whole generated pool on THIS GPU by another
+    code path: the pool regenerated chunk by chunk (make_pool's global
+    chunks) and streamed through one running top-q (ops.MCChunkJob).  Outside
+    the timed region; ~1 s at 100M items."""
+    from ce_amd import ops
+
+    job = ops.MCChunkJob(q, layout, device)
+    for lo in range(0, N, POOL_CHUNK):
+        hi = min(N, lo + POOL_CHUNK)
+        P = make_pool(lo, hi, M, C, device)
+        if layout == "MNC":
+            P = P.permute(1, 0, 2).contiguous()
+        job.add(P, lo)
+        del P
+    _, idx = job.result()
+    return idx.cpu().tolist()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -254,13 +390,17 @@ def main():
     ap.add_argument("--layout", default="NMC", choices=["NMC", "MNC"])
     ap.add_argument("--cpu-sample", type=int, default=6_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-n1-check", action="store_true", help="skip the N=1 re-selection of the pool")
     args = ap.parse_args()
 
+    # before ANY GPU call: a plain `python3 bench.py --gpus N` starts N ranks itself
+    mode, world = launch_plan(args.gpus, os.environ, torch.cuda.device_count())
+    if mode == "spawn":
+        log(f"bench.py: starting {world} ranks (one process per GPU)")
+        sys.exit(spawn_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], world))
+
     rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
     # CE_AMD_REHEARSAL=1: several ranks share the visible GPUs over gloo (a
     # one-GPU rehearsal of the multi-GPU code path; never used for a bench line)
     rehearsal = os.environ.get("CE_AMD_REHEARSAL") == "1"
@@ -332,9 +472,30 @@ def main():
     kern_ms = statistics.mean(a.elapsed_time(b) for a, b in ev)
     picks = idx.cpu().tolist()
     launched = ce_amd._lib.load().ce_last_kernel().decode()  # the stage-1 kernel of the last step
+    backend = dist.get_backend() if world > 1 else None
+
+    bytes_per_launch = n_local * M * C * P.element_size()
+    # release the pool before the checks below (the N=1 re-selection and the
+    # CPU baseline): only the selected positions are needed from here on
+    del step, P
+    plan = sstep = None  # noqa: F841
+    torch.cuda.empty_cache()
+
+    check = None
+    if rank == 0:
+        # the ranks' merged selection vs the N=1 selection of the same pool
+        # (after the timed region): the committed 1-GPU record when there is
+        # one for this workload, and a re-selection on this GPU by the chunked
+        # single-GPU path
+        rec = recorded_selection(f"{args.layout}_{N}_{M}_{C}_q{q}")
+        n1 = None if args.no_n1_check else n1_selection(N, M, C, q, args.layout, device)
+        check = {"n1_rechecked": None if n1 is None else n1 == picks,
+                 "n1_record": None if rec is None else rec == picks,
+                 "record": os.path.relpath(SELECTED_FILE, ROOT) if rec is not None else None,
+                 "method": "rank 0 regenerated the whole pool in 4M-item chunks and streamed it through "
+                           "ops.MCChunkJob (one GPU, one running top-q), after the timed region"}
 
     if rank == 0:
-        bytes_per_launch = n_local * M * C * P.element_size()
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = recorded_traffic(f"{args.layout}_{N}_{M}_{C}_q{q}_w{world}", launched)
         line = {
@@ -370,20 +531,26 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
             "cpu_baseline": None,
+            "ranks": world,
+            "backend": backend,
             "selected": picks,
+            "selected_equal_n1": (None if check["n1_rechecked"] is None and check["n1_record"] is None
+                                  else check["n1_rechecked"] is not False and check["n1_record"] is not False),
+            "selected_check": check,
         }
         if rehearsal:  # ranks sharing one GPU over gloo: a code-path rehearsal, not a multi-GPU figure
             line["rehearsal"] = {"backend": "gloo", "gpus_visible": torch.cuda.device_count(),
                                  "note": "NOT a multi-GPU measurement"}
             line["value"] = None
         if world == 1 and not args.no_cpu_baseline:
-            del P, plan, step
-            torch.cuda.empty_cache()
             line["cpu_baseline"] = cpu_baseline(args.cpu_sample, M, C, q)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and line["selected_equal_n1"] is False:
+        log("bench.py: the selection differs from the N=1 selection of the same pool")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -17,6 +17,7 @@ except ImportError:  # pragma: no cover - torch is part of this image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
 # CE_AMD_LIB: an alternative build of the same ABI (A/B runs of kernel variants)
 LIB_PATH = os.environ.get("CE_AMD_LIB") or os.path.join(_HERE, "libce_amd.so")
 
@@ -85,28 +86,98 @@ class CEError(RuntimeError):
         self.code = code
 
 
+def source_hash(pkg_dir=_PKG):
+    """The content hash of the engine's sources in this tree, by the Makefile's
+    rule (SRC_HASH): sha256 over the sorted csrc/*.hip, csrc/*.hpp files, then
+    include/ce.h, concatenated; the first 16 hex digits.  None when the tree
+    holds no sources (an installed copy)."""
+    import hashlib
+
+    csrc = os.path.join(pkg_dir, "csrc")
+    header = os.path.join(os.path.dirname(pkg_dir), "include", "ce.h")
+    if not os.path.isdir(csrc) or not os.path.isfile(header):
+        return None
+    h = hashlib.sha256()
+    for f in sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".hpp"))) + [None]:
+        with open(header if f is None else os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def built_hash(version):
+    """The source hash a library embeds in ce_version() ("... src=<hash>"), or None."""
+    v = version.decode(errors="replace") if isinstance(version, bytes) else str(version)
+    return v.split("src=", 1)[1].split()[0] if "src=" in v else None
+
+
+def verify_source(lib, path, pkg_dir=_PKG, explicit=False):
+    """Refuse a library built from other sources than the tree's (a stale or
+    swapped build).  explicit (CE_AMD_LIB named the library on purpose): report
+    the difference on stderr instead."""
+    tree = source_hash(pkg_dir)
+    if tree is None:
+        return
+    got = built_hash(lib.ce_version())
+    if got == tree:
+        return
+    msg = (f"{path} was built from other sources (its ce_version() says src={got}, the tree's "
+           f"{os.path.join(pkg_dir, 'csrc')} + include/ce.h hash to {tree})")
+    if explicit:
+        import sys
+
+        print(f"ce_amd: note: CE_AMD_LIB: {msg}", file=sys.stderr)
+        return
+    raise RuntimeError(f"stale HIP extension: {msg}; rebuild it (`make -C consensus-entropy_amd`). "
+                       "There is no CPU fallback.")
+
+
 def load():
-    """Load libce_amd.so.  Raises (never falls back) when it is missing."""
+    """Load libce_amd.so.  Raises (never falls back) when it is missing or was
+    built from other sources than the tree's (ce_version() hash, verify_source)."""
     global _lib
     with _lock:
         if _lib is None:
+            explicit = bool(os.environ.get("CE_AMD_LIB"))
             if not os.path.exists(LIB_PATH):
                 raise RuntimeError(
                     f"HIP extension not built: {LIB_PATH} is missing "
                     "(run `python -c 'import __graft_entry__ as g; g.build()'` or "
                     "`make -C consensus-entropy_amd`). There is no CPU fallback.")
             lib = ctypes.CDLL(LIB_PATH)
+            missing = []
             for name, (res, args) in SIGNATURES.items():
                 try:
                     f = getattr(lib, name)
                 except AttributeError:
-                    if os.environ.get("CE_AMD_LIB"):  # an older A/B build: bind what it exports
+                    if explicit:  # an older A/B build: bind what it exports, and say what it lacks
+                        missing.append(name)
                         continue
                     raise
                 f.restype = res
                 f.argtypes = args
+            if missing:
+                import sys
+
+                print(f"ce_amd: note: CE_AMD_LIB={LIB_PATH} lacks {', '.join(missing)}", file=sys.stderr)
+            verify_source(lib, LIB_PATH, explicit=explicit)
             _lib = lib
     return _lib
+
+
+_capture_info = None
+
+
+def hip_stream_capture_info(stream, status, capture_id):
+    """hipStreamGetCaptureInfo(stream, &status, &id) of the HIP runtime the
+    engine links (the one torch loaded): 0 = success.  The graph-workspace
+    cache keys a capture's workspace by this id (ops._WorkspaceCache)."""
+    global _capture_info
+    if _capture_info is None:
+        f = load().hipStreamGetCaptureInfo  # resolved through libce_amd.so's own dependency
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong)]
+        _capture_info = f
+    return _capture_info(ctypes.c_void_p(stream), ctypes.byref(status), ctypes.byref(capture_id))
 
 
 def call(name, *args):

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -50,6 +51,64 @@ def new_workspace(nbytes, device, header_only=False):
     return buf
 
 
+class _GraphArena:
+    """Zero-filled device memory that captured selections carve their
+    workspaces from, one arena per device, filled and synchronised ONCE,
+    eagerly, outside any capture.
+
+    A captured call's workspace header (the arrival counters) must be zero at
+    the graph's first replay; every call leaves it zero again (include/ce.h).
+    Carving from memory zeroed before the capture therefore needs no zero-fill
+    node in the graph: each replay runs the selection kernel alone.  A carve is
+    never handed out twice, and it is never freed, because a graph may replay
+    for the life of the process.  Captures are rare (one per graph) and a small
+    pool's workspace is 70-230 KB, so the default 64 MiB lasts hundreds of
+    captures.  reserve() adds room before a capture that needs more."""
+
+    ALIGN = 256
+    DEFAULT_BYTES = int(os.environ.get("CE_AMD_GRAPH_ARENA_MB", "64")) << 20
+
+    def __init__(self):
+        self._free = {}  # device index -> list of [buffer, next offset]
+
+    def reserve(self, device, nbytes):
+        """Eager only: make sure `nbytes` can be carved on `device` (adds a
+        new zeroed arena when the current ones are short)."""
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("reserve_graph_workspace must run outside HIP-graph capture")
+        arenas = self._free.setdefault(device.index, [])
+        if any(buf.numel() - off >= nbytes for buf, off in arenas):
+            return
+        n = max(int(nbytes) + self.ALIGN, self.DEFAULT_BYTES)
+        buf = torch.zeros(n, dtype=torch.uint8, device=device)
+        # the one synchronisation: the fill must be done before any replay,
+        # and a replay may run on any stream
+        torch.cuda.current_stream(device).synchronize()
+        arenas.append([buf, 0])
+
+    def ensure(self, device):
+        if device.index not in self._free:
+            self.reserve(device, 0)
+
+    def carve(self, device, nbytes):
+        """A zero-filled region of >= nbytes that nothing else uses, or None."""
+        nbytes = max(int(nbytes), 256)
+        for slot in self._free.get(device.index, ()):
+            buf, off = slot
+            if buf.numel() - off >= nbytes:
+                slot[1] = off + (nbytes + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+                return buf[off:off + nbytes]
+        return None
+
+
+def _capture_id(device):
+    """The HIP capture id of the device's current stream (unique per capture)."""
+    st = ctypes.c_int(0)
+    cid = ctypes.c_ulonglong(0)
+    rc = _lib.hip_stream_capture_info(torch.cuda.current_stream(device).cuda_stream, st, cid)
+    return cid.value if rc == 0 else None
+
+
 class _WorkspaceCache:
     """Scratch reused across calls, one per (device, stream): include/ce.h
     allows one workspace per stream -- its header holds the arrival counters of
@@ -64,11 +123,16 @@ class _WorkspaceCache:
     released when the call's tensors are, so one large-q call does not keep
     them allocated for the life of the process.
 
-    Under HIP-graph capture every call gets a FRESH zero-filled workspace
-    allocated inside the capture (from the graph's private pool; its zero fill
-    is a captured memset that runs at every replay): a graph never references a
-    cached buffer, so growing the cache later cannot free memory a graph still
-    uses, and replays never share counters with eager calls."""
+    Under HIP-graph capture a call never uses a cached buffer, so growing the
+    cache later cannot free memory a graph still uses, and replays never share
+    counters with eager calls.  The workspace is carved from the pre-zeroed
+    graph arena (_GraphArena): one carve per (capture, stream), shared by the
+    sequential calls on that stream inside that capture, as eager calls share
+    their stream's buffer.  The replays then run no zero-fill node.  When the
+    arena has no room (or no eager call ever created it), the call falls back
+    to a workspace allocated inside the capture with a captured zero fill that
+    runs at every replay (correct, one node slower; warned once).  Sort-path
+    calls under capture always take that fallback with a header-only fill."""
 
     MAX_STREAMS = 16
 
@@ -76,6 +140,9 @@ class _WorkspaceCache:
         import collections
 
         self._ws = collections.OrderedDict()
+        self._captured = {}  # (device, stream, capture id) -> carved workspace
+        self.arena = _GraphArena()
+        self._warned = False
 
     def get(self, device, nbytes, transient=False):
         device = torch.device(device)
@@ -84,9 +151,10 @@ class _WorkspaceCache:
         with torch.cuda.device(device):  # the capture state of THIS device's current stream
             capturing = torch.cuda.is_current_stream_capturing()
         if capturing:
-            return new_workspace(nbytes, device)
+            return self._get_captured(device, nbytes, transient)
         if transient:
             return new_workspace(nbytes, device, header_only=True)
+        self.arena.ensure(device)
         key = (device.index, torch.cuda.current_stream(device).cuda_stream)
         buf = self._ws.get(key)
         if buf is None or buf.numel() < nbytes:
@@ -99,11 +167,47 @@ class _WorkspaceCache:
             self._ws.popitem(last=False)
         return buf
 
+    def _get_captured(self, device, nbytes, transient):
+        if not transient:
+            cid = _capture_id(device)
+            key = (device.index, torch.cuda.current_stream(device).cuda_stream, cid)
+            buf = self._captured.get(key) if cid is not None else None
+            if buf is not None and buf.numel() >= nbytes:
+                return buf
+            buf = self.arena.carve(device, nbytes) if cid is not None else None
+            if buf is not None:
+                self._captured[key] = buf
+                return buf
+            if not self._warned:
+                import warnings
+
+                warnings.warn("ce_amd: no pre-zeroed graph workspace left (call ops.reserve_graph_workspace "
+                              "before capture); this captured selection replays a zero-fill node", stacklevel=3)
+                self._warned = True
+        return new_workspace(nbytes, device, header_only=transient)
+
+    def clear(self):
+        """Release the cached eager workspaces (the graph arena stays: graphs
+        may still replay from it)."""
+        self._ws.clear()
+
     def __len__(self):
         return len(self._ws)
 
 
 WORKSPACE = _WorkspaceCache()
+
+
+def reserve_graph_workspace(nbytes, device=None):
+    """Before capturing selections into a HIP graph: make sure the graph arena
+    can hand out `nbytes` of pre-zeroed workspace on `device` (eager only).
+    Size it with the ce_*_workspace_bytes functions, one carve per stream per
+    capture."""
+    device = torch.device(device if device is not None else "cuda")
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    with torch.cuda.device(device):
+        WORKSPACE.arena.reserve(device, int(nbytes))
 
 
 def committee_view(P, layout="MNC"):

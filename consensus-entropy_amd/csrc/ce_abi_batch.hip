@@ -14,6 +14,7 @@ extern "C" size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t 
 extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
                              int64_t sC, const double* hc, int64_t N_h, int64_t ld_hc, int32_t q, void* ws,
                              size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
     int rc = check_comm(a);
     if (rc) return rc;
@@ -91,6 +92,7 @@ extern "C" size_t ce_select_batched_workspace_bytes(int64_t total_items, int32_t
 extern "C" int ce_select_batched(const void* p, ce_dtype dt, int64_t total_items, int32_t M, int32_t C, int64_t sN,
                                  int64_t sM, int64_t sC, const int64_t* offsets, int32_t U, int32_t q, void* ws,
                                  size_t ws_bytes, double* val_out, int64_t* idx_out, ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     CommArgs a{p, (int)dt, total_items, M, C, sN, sM, sC};
     int rc = check_comm(a);
     if (rc) return rc;

@@ -123,6 +123,7 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
 extern "C" int ce_select_mc_cands(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,
                                   int64_t sC, int32_t q, int64_t base_idx, void* ws, size_t ws_bytes, ce_cand* out,
                                   ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     CommArgs a{p, (int)dt, N, M, C, sN, sM, sC};
     int rc = check_comm(a);
     if (rc) return rc;
@@ -156,6 +157,7 @@ extern "C" int ce_select_mc_cands(const void* p, ce_dtype dt, int64_t N, int32_t
 extern "C" int ce_select_mc_partial(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
                                     int64_t sM, int64_t sC, int32_t q, int64_t base_idx, void* ws,
                                     size_t ws_bytes, ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     if (q > CE_MAX_Q)
         return fail(CE_EUNSUPPORTED, "two-stage selection needs q <= %d (ce_select_mc takes any q)", CE_MAX_Q);
     if (q <= 0) return check_q(q);
@@ -169,6 +171,7 @@ extern "C" int ce_select_mc_partial(const void* p, ce_dtype dt, int64_t N, int32
 
 extern "C" int ce_select_finish(int64_t N, int32_t q, void* ws, size_t ws_bytes, double* val_out, int64_t* idx_out,
                                 ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     int rc = check_q(q);
     if (rc) return rc;
     if (q > CE_MAX_Q)
@@ -186,6 +189,7 @@ static_assert(sizeof(ce_cand) == sizeof(Cand) && alignof(ce_cand) <= alignof(Can
 
 extern "C" int ce_select_finish_cands(int64_t N, int32_t q, void* ws, size_t ws_bytes, ce_cand* out,
                                       ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     int rc = check_q(q);
     if (rc) return rc;
     if (q > CE_MAX_Q)
@@ -202,6 +206,7 @@ extern "C" int ce_select_finish_cands(int64_t N, int32_t q, void* ws, size_t ws_
 
 extern "C" int ce_merge_cands(const ce_cand* c, int32_t nlists, int32_t q, double* val_out, int64_t* idx_out,
                               ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     int rc = check_q(q);
     if (rc) return rc;
     if (q == 0) return CE_OK;
@@ -233,6 +238,7 @@ extern "C" size_t ce_select_mc_chunk_workspace_bytes(int64_t N, int32_t q) {
 extern "C" int ce_select_mc_chunk(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN,
                                   int64_t sM, int64_t sC, int32_t q, int64_t base_idx, ce_cand* running,
                                   int32_t first, void* ws, size_t ws_bytes, ce_stream_t stream) {
+    note_kernel("%s", "");  // ce_last_kernel(): "" unless this call notes a kernel
     int rc = check_q(q);
     if (rc) return rc;
     if (q == 0) return CE_OK;

@@ -69,7 +69,7 @@ const char *ce_last_error(void);
 const char *ce_version(void);
 /* The main kernel the last selection call on this thread launched, as
  * rocprofv3 names it without "void " and the argument list (e.g.
- * "ce::k_stream_nmc<0, 4, 16, 2, false>"); "" when that call launched none
+ * "ce::k_stream_nmc<0, 4, 16, 2, false, 2>"); "" when that call launched none
  * of the noted kernels.  Lets a benchmark tie a profiled figure to the kernel
  * it actually ran. */
 const char *ce_last_kernel(void);

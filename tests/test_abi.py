@@ -87,3 +87,50 @@ def test_no_cpu_fallback():
 
     with pytest.raises(ValueError, match="HIP device"):
         ops.select_mc(torch.zeros((4, 8, 4)), 2)
+
+
+def test_library_embeds_the_tree_source_hash():
+    """libce_amd.so carries the content hash of the sources it was built from
+    (ce_version() "src=..."), equal to the tree's (the Makefile's rule)."""
+    from ce_amd import _lib
+
+    lib = _lib.load()
+    assert _lib.built_hash(lib.ce_version()) == _lib.source_hash() is not None
+
+
+def _copy_tree(tmp_path):
+    import shutil
+
+    pkg = tmp_path / "consensus-entropy_amd"
+    shutil.copytree(os.path.join(PKG_DIR, "ce_amd"), pkg / "ce_amd",
+                    ignore=shutil.ignore_patterns("__pycache__"))
+    shutil.copytree(os.path.join(PKG_DIR, "csrc"), pkg / "csrc")
+    shutil.copytree(os.path.join(ROOT, "include"), tmp_path / "include")
+    return pkg
+
+
+def _load_in(pkg, extra_env=None):
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k != "CE_AMD_LIB"}
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, "-c", "import ce_amd; ce_amd.load(); print('loaded')"], cwd=str(pkg),
+                          capture_output=True, text=True, timeout=300, env=env)
+
+
+def test_load_refuses_a_stale_library(tmp_path):
+    """One byte flipped in a copied header makes the copied library stale:
+    load() refuses it (no silent use of a build of other sources); the
+    unmodified copy loads; CE_AMD_LIB naming the library on purpose only
+    reports the difference on stderr."""
+    pkg = _copy_tree(tmp_path)
+    ok = _load_in(pkg)
+    assert ok.returncode == 0 and "loaded" in ok.stdout, ok.stderr[-1500:]
+    hdr = pkg / "csrc" / "ce_device.hpp"
+    b = bytearray(hdr.read_bytes())
+    b[100] ^= 0x01
+    hdr.write_bytes(bytes(b))
+    bad = _load_in(pkg)
+    assert bad.returncode != 0 and "stale HIP extension" in bad.stderr, bad.stderr[-1500:]
+    swapped = _load_in(pkg, {"CE_AMD_LIB": str(pkg / "ce_amd" / "libce_amd.so")})
+    assert swapped.returncode == 0 and "built from other sources" in swapped.stderr, swapped.stderr[-1500:]

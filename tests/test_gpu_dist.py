@@ -130,6 +130,9 @@ def test_bench_contract_small():
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] in ("port", "reference")
     assert len(line["selected"]) == 10
+    assert line["ranks"] == 1 and line["selected_equal_n1"] is True
+    assert line["selected_check"]["n1_rechecked"] is True and line["selected_check"]["n1_record"] is None
+    assert cb["kind"] == "reference"
 
 
 def test_rccl_sharded_mix_and_batched_world1():
@@ -202,3 +205,15 @@ def test_bench_world2_rehearsal():
     assert l2["rehearsal"]["backend"] == "gloo" and l2["value"] is None  # never a valid-looking multi-GPU figure
     assert "rehearsal" not in l1 and l1["value"] > 0
     assert l1["selected"] == l2["selected"] and len(l1["selected"]) == 10
+    assert l2["ranks"] == 2 and l2["backend"] == "gloo" and l2["selected_equal_n1"] is True
+    assert l1["ranks"] == 1 and l1["backend"] is None and l1["selected_equal_n1"] is True
+    # the same without torchrun: a plain `bench.py --gpus 2` starts both ranks itself
+    three = subprocess.run([sys.executable] + args[:1] + ["--gpus", "2"] + args[1:], cwd=root, capture_output=True,
+                           text=True, timeout=600, env=env2)
+    assert three.returncode == 0, three.stderr[-2000:]
+    lines = [ln for ln in three.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0's line only
+    l3 = json.loads(lines[0])
+    assert l3["n_gpus"] == 2 and l3["ranks"] == 2 and l3["config"]["items_per_gpu"] == 1500001
+    assert l3["selected"] == l1["selected"] and l3["selected_equal_n1"] is True
+    assert l3["selected_check"]["n1_rechecked"] is True and l3["value"] is None

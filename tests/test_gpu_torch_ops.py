@@ -53,6 +53,78 @@ def test_hip_graph_capture(tops):
     assert torch.equal(i, ie)
 
 
+def _graph_nodes(g):
+    """Node count of a kept (keep_graph=True) captured graph."""
+    import ctypes
+
+    import ce_amd
+
+    f = ce_amd._lib.load().hipGraphGetNodes
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+    n = ctypes.c_size_t(0)
+    assert f(ctypes.c_void_p(g.raw_cuda_graph()), None, ctypes.byref(n)) == 0
+    return n.value
+
+
+def test_graph_replays_1000_without_zero_fill(tops):
+    """A captured select_mc (and select_batched / select_mix, sharing one
+    carve on the capture stream) replayed 1000x equals the oracle on fresh
+    pools: the workspace comes from the pre-zeroed graph arena (no zero-fill
+    node in the graph, no fallback warning) and every replay leaves the
+    arrival counters zero for the next."""
+    import warnings
+
+    import ce_amd.ops as ops
+    from oracle import ce_oracle as O
+
+    P = pool(71, (4, 1608, 4))
+    Pb = pool(72, (4, 40 * 1608, 4))
+    hc = torch.round(pool(73, (1608, 4)).double() * 1000) / 1000
+    offs = torch.arange(0, 41, device="cuda", dtype=torch.int64) * 1608
+    ops.select_mc(P, 10, "MNC")  # an eager call first: it creates the device's graph arena
+    ops.reserve_graph_workspace(4 << 20)
+    torch.cuda.synchronize()
+
+    def capture():
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(g):
+            out = (ops.select_mc(P, 10, "MNC"), ops.select_batched(Pb, offs, 10, "MNC"),
+                   ops.select_mix(P, hc, 10, "MNC"))
+        g.instantiate()
+        return g, out
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # the fallback (a captured zero fill) warns
+        g, ((v, i), (vb, ib), (vm, im)) = capture()
+    carve = ops.WORKSPACE.arena.carve
+    ops.WORKSPACE.arena.carve = lambda *a: None  # force the fallback: one zero fill per call
+    try:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            g_fill, _ = capture()
+    finally:
+        ops.WORKSPACE.arena.carve = carve
+    n_arena, n_fill = _graph_nodes(g), _graph_nodes(g_fill)
+    assert n_fill == n_arena + 3, (n_arena, n_fill)  # the arena's graph: the selection kernels only
+    del g_fill
+    for it in range(1000):
+        if it % 250 == 0:
+            P.copy_(pool(100 + it, P.shape))
+            Pb.copy_(pool(200 + it, Pb.shape))
+        g.replay()
+        if it % 250 == 249 or it == 0:
+            torch.cuda.synchronize()
+            Pn = P.cpu().numpy().astype(np.float64)
+            assert np.array_equal(i.cpu().numpy(), O.oracle_select_mc(Pn, 10)[1])
+            assert np.array_equal(im.cpu().numpy(), O.oracle_select_mix(Pn, hc.cpu().numpy(), 10)[1])
+            Pbn = Pb.cpu().numpy().astype(np.float64)
+            for u in (0, 17, 39):
+                eu = O.oracle_select_mc(np.ascontiguousarray(Pbn[:, u * 1608:(u + 1) * 1608]), 10)[1]
+                assert np.array_equal(ib[u].cpu().numpy(), eu)
+    torch.cuda.synchronize()
+
+
 def test_dynamo_traces_one_node(tops):
     P = pool(4, (4, 5_000, 4))
     hc = pool(5, (5_000, 4)).double()
@@ -178,6 +250,16 @@ def test_last_kernel_names_the_stage1_kernel(tops):
     ops.select_mc(small, 10, "MNC")
     assert lib.ce_last_kernel().decode().startswith("ce::k_select_tiles<ce::CommitteeSrc<0, 4, true>")
     ops.select_mc(P, 100, "NMC")  # q > 64: the block-synchronous lists, not a noted kernel
+    assert lib.ce_last_kernel().decode() == ""
+    # every selection entry point resets the name: a sort-path call after a noted one reports ""
+    ops.select_mc(P, 10, "NMC")
+    assert lib.ce_last_kernel().decode() != ""
+    offs = torch.tensor([0, 100_000, 200_000], device="cuda", dtype=torch.int64)
+    ops.select_batched(P.permute(1, 0, 2), offs, 3000, "MNC")
+    assert lib.ce_last_kernel().decode() == ""
+    ops.select_mc(P, 10, "NMC")
+    ent = ops.committee_entropy(P, "NMC")
+    ops.topq(ent, 3000)
     assert lib.ce_last_kernel().decode() == ""
     torch.cuda.synchronize()
 

@@ -220,3 +220,75 @@ def test_committed_traffic_records_name_a_kernel():
         assert e["kernel"].startswith("void ce::k_") and "(" in e["kernel"], key
         assert e["hbm_bytes_per_launch"] > 0 and e["source"].startswith("profiles/"), key
         assert "k_stream_direct" not in e["kernel"], key
+
+
+def test_bench_launch_plan():
+    """bench.py --gpus N: one rank under torchrun (WORLD_SIZE set), N child
+    ranks started by bench.py itself otherwise, and a refusal -- never a
+    1-GPU line -- for a --gpus that WORLD_SIZE contradicts or that exceeds
+    the visible GPUs outside a rehearsal."""
+    import bench
+
+    assert bench.launch_plan(1, {}, 0) == ("run", 1)  # N = 1 (the CPU box: the GPU call fails later, loudly)
+    assert bench.launch_plan(1, {}, 8) == ("run", 1)
+    assert bench.launch_plan(8, {}, 8) == ("spawn", 8)
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}, 8) == ("run", 8)
+    assert bench.launch_plan(2, {"CE_AMD_REHEARSAL": "1"}, 1) == ("spawn", 2)
+    assert bench.launch_plan(2, {"WORLD_SIZE": "2", "CE_AMD_REHEARSAL": "1"}, 1) == ("run", 2)
+    for gpus, env, vis in ((8, {}, 1), (2, {"WORLD_SIZE": "1"}, 8), (1, {"WORLD_SIZE": "8"}, 8),
+                           (8, {"WORLD_SIZE": "8"}, 4), (0, {}, 8)):
+        with pytest.raises(SystemExit) as e:
+            bench.launch_plan(gpus, env, vis)
+        assert e.value.code == 2, (gpus, env, vis)
+    env = bench.rank_env({"X": "1"}, 3, 8, 12345)
+    assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"], env["MASTER_ADDR"], env["MASTER_PORT"], env["X"]) == \
+        ("3", "3", "8", "127.0.0.1", "12345", "1")
+
+
+def test_bench_refuses_without_gpus():
+    """A plain `python3 bench.py --gpus 2` with no visible GPU exits 2 and
+    prints no JSON line (here: the CPU container)."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "CE_AMD_REHEARSAL")}
+    env["HIP_VISIBLE_DEVICES"] = "-1" if env.get("HIP_VISIBLE_DEVICES") is None else env["HIP_VISIBLE_DEVICES"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "64"], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 2 and r.stdout.strip() == "", (r.returncode, r.stdout, r.stderr[-500:])
+    assert "visible GPU" in r.stderr
+
+
+def test_bench_spawn_ranks_env_and_status(tmp_path):
+    """bench.spawn_ranks starts N fresh processes with torchrun's variables
+    (rank, world, one free 127.0.0.1 port) and returns the worst status: the
+    failing rank's, 128 + signal for a killed one, 0 when all succeed."""
+    import json
+    import sys
+
+    import bench
+
+    child = tmp_path / "child.py"
+    child.write_text(
+        "import json, os, sys\n"
+        "e = os.environ\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'r' + e['RANK']), 'w').write(json.dumps(\n"
+        "    {k: e[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')}))\n"
+        "sys.exit(7 if e.get('FAIL_RANK') == e['RANK'] else 0)\n")
+    code = str(child)
+    assert bench.spawn_ranks([sys.executable, code], 3, poll_s=0.05) == 0
+    seen = [json.loads((tmp_path / f"r{r}").read_text()) for r in range(3)]
+    assert [s["RANK"] for s in seen] == ["0", "1", "2"] and {s["WORLD_SIZE"] for s in seen} == {"3"}
+    assert {s["MASTER_ADDR"] for s in seen} == {"127.0.0.1"} and len({s["MASTER_PORT"] for s in seen}) == 1
+    import os
+
+    os.environ["FAIL_RANK"] = "1"
+    try:
+        assert bench.spawn_ranks([sys.executable, code], 3, poll_s=0.05) == 7
+    finally:
+        del os.environ["FAIL_RANK"]
+    kill = "import os, signal; os.kill(os.getpid(), signal.SIGKILL) if os.environ['RANK'] == '0' else None"
+    assert bench.spawn_ranks([sys.executable, "-c", kill], 2, poll_s=0.05) == 128 + 9

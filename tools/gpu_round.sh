@@ -181,6 +181,7 @@ gather)  # SURVEY §8(f)1 shuffled frames: the random-row probe + FETCH / WRITE 
   step $? "gather write"
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof/gather_trace" -o run --output-format csv -- python3 "$ROOT/tools/gather_probe.py" --pmc > "$OUT/gather_trace.log" 2>&1
   step $? "gather trace"
+  [ -x "$ROOT/tools/_diag/random_row_probe" ] || { echo "build it first: make -C consensus-entropy_amd probes" >> "$LOG"; exit 2; }
   timeout -k 10 120 "$ROOT/tools/_diag/random_row_probe" > "$OUT/random_rows.json" 2> "$OUT/random_rows.err"
   step $? "random row probe"
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof/rows32_fetch" -o run --output-format csv -- "$ROOT/tools/_diag/random_row_probe" 32 > "$OUT/rows32_fetch.log" 2>&1

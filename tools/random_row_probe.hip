@@ -5,7 +5,7 @@
 // S/8 lanes read one row (8 B per lane, as k_frames_lanes' shuffled path
 // does), 8 rows in flight per lane; row index = an odd-multiplier hash of the
 // ordinal mod 2^k (a bijection: every row read once per sweep).
-// Build: hipcc --offload-arch=gfx950 -O3 tools/random_row_probe.hip -o tools/_diag/random_row_probe
+// Build: make -C consensus-entropy_amd probes   (-> tools/_diag/random_row_probe, untracked)
 // Run:   tools/_diag/random_row_probe [S]   (one line per row size: rows/s, useful GB/s)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
