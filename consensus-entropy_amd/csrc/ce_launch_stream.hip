@@ -29,6 +29,9 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
 // items (M x C x size bytes) from which the wide stream runs one block per CU
 // with a deep register ring (below)
 constexpr int64_t kWideHeavyBytes = 16384;
+#ifndef CE_WIDE_HEAVY
+#define CE_WIDE_HEAVY 0
+#endif
 
 bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                    const uint32_t* excl) {
@@ -135,8 +138,13 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             // without the prefilter) the same grid reads 0.56 against 0.78, so the
             // first chunk and single selections keep the occupancy grid.
             bool heavy = false;
-            if constexpr (KCH <= 2)  // (wider lanes: 8 batches would spill)
+            if constexpr (KCH <= 2) {  // (wider lanes: 8 batches would spill)
+#if CE_WIDE_HEAVY == 1  // A/B: every long pool (>= 256 items per wave) on the deep-ring grid
+                heavy = R >= kWideHeavyBytes && a.N >= 1024 * (int64_t)device_cus() && CE_WIDE_PREFILTER;
+#else
                 heavy = R >= kWideHeavyBytes && fold != nullptr && fold->extra != nullptr && CE_WIDE_PREFILTER;
+#endif
+            }
             if (heavy) {
                 if constexpr (KCH <= 2) {
                     if (unr == UNR) go(k_stream_wide2<DT, KCH, UNR, 8>, 8, 1);

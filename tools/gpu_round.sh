@@ -15,6 +15,7 @@
 #   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
+#   PHASE=c5probe    tools/c5_probe.py per library build (LIBS="base x"), alternating (wide stream: iid vs rising pools)
 #   PHASE=gather     tools/gather_probe.py + FETCH / WRITE passes of the shuffled-frames kernel
 #   PHASE=framesab   tools/gather_probe.py per library build (LIBS="base x"), alternating
 #   PHASE=scale      tools/scale_proxy.py (per-rank proxies; world-1 RCCL step eager vs HIP graph)
@@ -205,10 +206,19 @@ memab)  # member-inference configs (bench_configs.py --only 6: GNB, SGD) per lib
     done
   done
   ;;
+c5probe)  # tools/c5_probe.py per library build (LIBS="base x"), alternating, REPS rounds (prefilter-friendly and rising pools)
+  for rep in $(seq 1 ${REPS:-2}); do
+    for lib in ${LIBS:-base}; do
+      if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
+      CE_AMD_LIB=$L timeout -k 10 300 python3 tools/c5_probe.py ${C5_ARGS} > "$OUT/c5probe${TAG}_${lib}_$rep.json" 2> "$OUT/c5probe${TAG}_${lib}_$rep.err"
+      step $? "c5probe $lib $rep"
+    done
+  done
+  ;;
 firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather, framesab, memab or tests" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather, framesab, memab, c5probe or tests" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
