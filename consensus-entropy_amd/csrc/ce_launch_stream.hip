@@ -32,6 +32,16 @@ constexpr int64_t kWideHeavyBytes = 16384;
 #ifndef CE_WIDE_HEAVY
 #define CE_WIDE_HEAVY 0
 #endif
+// the wave-pair wide stream (k_stream_wide_pair) for rows of 65..128 16-B chunks
+#ifndef CE_WIDE_PAIR
+#define CE_WIDE_PAIR 0
+#endif
+#ifndef CE_WIDE_PAIR_NB
+#define CE_WIDE_PAIR_NB 8
+#endif
+#ifndef CE_WIDE_PAIR_PER_CU
+#define CE_WIDE_PAIR_PER_CU 4
+#endif
 
 bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                    const uint32_t* excl) {
@@ -137,6 +147,30 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             // hide exact entropies, though: with every item exact (the build
             // without the prefilter) the same grid reads 0.56 against 0.78, so the
             // first chunk and single selections keep the occupancy grid.
+#if CE_WIDE_PAIR
+            // a pair of waves per item (k_stream_wide_pair): rows of 65..128 16-B chunks
+            if constexpr (KCH == 2) {
+                const int K = a.C / ChunkT<DT>::CPC;
+                if (R >= kWideHeavyBytes && K > 64 && K <= 128 && sa.excl == nullptr) {
+                    const size_t plds = 2 * (size_t)wide_lds_doubles(a.C) * sizeof(double);
+                    auto pgo = [&](auto kern, int unr_) {
+                        note_kernel("ce::k_stream_wide_pair<%d, %d, %d>", DT, unr_, CE_WIDE_PAIR_NB);
+                        int per_cu = 0;
+                        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 128, plds) != hipSuccess ||
+                            per_cu < 1)
+                            per_cu = 1;
+                        (void)hipGetLastError();
+                        per_cu = std::min(per_cu, CE_WIDE_PAIR_PER_CU);
+                        const int grid = std::min(per_cu * device_cus(), G);
+                        sa.nlists = G;
+                        hipLaunchKernelGGL(kern, dim3(grid), dim3(128), plds, st, wa, pl, sa, q, w.c);
+                    };
+                    if (a.M % 4 == 0) pgo(k_stream_wide_pair<DT, 4, CE_WIDE_PAIR_NB>, 4);
+                    else pgo(k_stream_wide_pair<DT, 1, CE_WIDE_PAIR_NB>, 1);
+                    return;
+                }
+            }
+#endif
             bool heavy = false;
             if constexpr (KCH <= 2) {  // (wider lanes: 8 batches would spill)
 #if CE_WIDE_HEAVY == 1  // A/B: every long pool (>= 256 items per wave) on the deep-ring grid

@@ -15,6 +15,7 @@
 #   PHASE=debug      pytest -m gpu on the debug build (CE_DASSERT device bounds checks)
 #   PHASE=phase      per-block phase stamps of C3 on the diagnostic build (make phase)
 #   PHASE=firstcall  first-call latency per library build (tools/first_call.py)
+#   PHASE=c3drain    rocprofv3 of tools/c3_drain_probe.hip (configs[2] reads only: the load floor)
 #   PHASE=c5probe    tools/c5_probe.py per library build (LIBS="base x"), alternating (wide stream: iid vs rising pools)
 #   PHASE=gather     tools/gather_probe.py + FETCH / WRITE passes of the shuffled-frames kernel
 #   PHASE=framesab   tools/gather_probe.py per library build (LIBS="base x"), alternating
@@ -206,6 +207,12 @@ memab)  # member-inference configs (bench_configs.py --only 6: GNB, SGD) per lib
     done
   done
   ;;
+c3drain)  # the configs[2] load floor (tools/c3_drain_probe.hip: reads only, no selection) under rocprofv3
+  [ -x "$ROOT/tools/_diag/c3_drain_probe" ] || { echo "build it first: make -C consensus-entropy_amd probes" >> "$LOG"; exit 2; }
+  cd /tmp
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof/${TAG}c3drain" -o run --output-format csv -- "$ROOT/tools/_diag/c3_drain_probe" 200 > "$OUT/${TAG}c3drain.json" 2> "$OUT/${TAG}c3drain.err"
+  step $? "c3 drain probe"
+  ;;
 c5probe)  # tools/c5_probe.py per library build (LIBS="base x"), alternating, REPS rounds (prefilter-friendly and rising pools)
   for rep in $(seq 1 ${REPS:-2}); do
     for lib in ${LIBS:-base}; do
@@ -219,6 +226,6 @@ firstcall)  # first-call latency per library build (tools/first_call.py)
   timeout -k 10 300 python3 tools/first_call.py ${LIBS} > "$OUT/first_call.json" 2> "$OUT/first_call.err"
   step $? "first call"
   ;;
-*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather, framesab, memab, c5probe or tests" >&2; exit 2 ;;
+*) echo "PHASE must be check, ab, profile, benchprof, configs, xgb, mpmc, small, c5, c5ab, smallab, debug, phase, firstcall, scale, gather, framesab, memab, c5probe, c3drain or tests" >&2; exit 2 ;;
 esac
 echo "done $PHASE $(date)" >> "$LOG"
