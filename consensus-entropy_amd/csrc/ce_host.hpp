@@ -210,6 +210,8 @@ static inline StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx)
     s.oidx = nullptr;
     s.ocand = nullptr;
     s.extra = nullptr;
+    s.vote = nullptr;
+    s.vote_heavy = 0;
     return s;
 }
 
@@ -244,6 +246,7 @@ struct FoldOut {
     int64_t* oidx;
     Cand* ocand;
     const Cand* extra;  // one more list to merge (a chunked job's running list), or nullptr
+    uint32_t* vote;     // with extra: a device word for the wide stream's grid vote (k_wide_vote), or nullptr
 };
 CE_HIDDEN int launch_stream_fold(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                                  const uint32_t* excl, FoldOut out);

@@ -350,9 +350,63 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 #ifndef CE_WIDE_PREFILTER
 #define CE_WIDE_PREFILTER 1
 #endif
+// A chunked job's seeded chunks choose their grid on the device (both grids
+// are launched, ce_launch_stream.hip): kWideVoteSamples items spread evenly
+// over the chunk, one wave each, take the prefilter's test against the running
+// list's q-th entry, and *vote counts the ones that would take the exact
+// entropy (every sample when the list is not full yet).  The deep-ring grid
+// (one block per CU, 8-batch ring) reads a chunk whose items nearly all skip
+// at 0.86-0.89 of HBM, but one whose items beat the running floor (e.g. a pool
+// ordered by rising entropy) at 0.51, where the occupancy grid keeps 0.79-0.82
+// (profiles/r06_c5_vote.json): it runs iff at most 1/kWideVoteDen of the
+// samples are exact.  The vote reads ~kWideVoteSamples items (64 MB of a
+// 128 GB C5 chunk).
+constexpr int kWideVoteSamples = 1024;
+constexpr int kWideVoteDen = 16;
+__device__ __forceinline__ bool wide_vote_heavy(uint32_t v, int64_t N) {
+    const int64_t ns = N < kWideVoteSamples ? N : kWideVoteSamples;
+    return (int64_t)v * kWideVoteDen <= ns;
+}
+template <int DT, int KCH, int UNR>
+__global__ __launch_bounds__(kBS) void k_wide_vote(WideArgs a, const Cand* __restrict__ extra, int q,
+                                                   uint32_t* __restrict__ vote) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t ns = a.N < kWideVoteSamples ? a.N : kWideVoteSamples;
+    const int64_t s = (int64_t)blockIdx.x * 4 + w;
+    if (s >= ns) return;  // wave-uniform
+    CE_DASSERT(q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
+    const Cand e = extra[q - 1];
+    bool exact = true;
+    if (e.idx >= 0 && e.key != 0) {
+        constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
+        const int K = a.C / CPC;
+        uint32_t off[KCH];
+#pragma unroll
+        for (int kk = 0; kk < KCH; ++kk) {
+            const int ch = lane + 64 * kk;
+            off[kk] = 16u * (uint32_t)(ch < K ? ch : K - 1);
+        }
+        const char* item = static_cast<const char*>(a.p) + (s * a.N / ns) * a.sN * EB;
+        double acc[KCH * CPC];
+#pragma unroll
+        for (int x = 0; x < KCH * CPC; ++x) acc[x] = 0.0;
+        WideBatch<DT, KCH, UNR> b;
+        for (int m = 0; m < a.M; m += UNR) {  // member order, as the stream adds
+            b.issue(item, m, a.sM * EB, off);
+            b.add(acc);
+        }
+        bool special;
+        const float ap = wave_approx_entropy<DT, KCH>(acc, K, special);
+        exact = special || !(e.key == ~0ull || (double)ap < key_to_val(e.key) * 1.4426950408889634 - 2.0 * kWideApproxErr2);
+    }
+    if (lane == 0 && exact) atomicAdd(vote, 1u);
+}
+
 template <int DT, int KCH, int UNR, int NB = 2>
 __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
+    // a seeded chunk's device-side grid choice (k_wide_vote): the other grid runs
+    if (sa.vote && wide_vote_heavy(*sa.vote, sa.N) != (sa.vote_heavy != 0)) return;
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     CE_DASSERT((int)gridDim.x <= sa.nlists && q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
     __shared__ WaveLists sm;
@@ -458,164 +512,6 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     }
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists, nullptr, nullptr, 4, sa.ctr != nullptr);
     if (sa.ctr) fold_merge<4>(sa.ctr, sa.oval, sa.oidx, sa.ocand, q, wc, sm, sa.extra);
-}
-
-// Wide classes, a PAIR of waves per item (q <= 64; member rows of <= 128
-// 16-B chunks, e.g. 1000 bf16 classes = 125 chunks): a 128-thread block = one
-// item stream; wave h owns chunks h*64 + lane of every member row, so each
-// class's member-sequential f64 sum stays in one lane (bit-identical to one
-// wave per item).  Both waves walk the same (item, member batch) sequence with
-// an NB-slot register ring (UNR member rows x one 16-B chunk per lane per
-// batch) and meet in LDS once an item's sums are complete:
-//   prefilter  each wave's f32 partial row sum and special flag, then its
-//              partial approximate entropy (the same bound as
-//              wave_approx_entropy: the partial sums add <= 1 rounding each);
-//   exact      the mean row (both waves' classes) in the block's LDS row A,
-//              the pairwise row sum (numpy's tree) by both waves, entr of
-//              each wave's classes into row B, the pairwise sum of row B --
-//              the same additions in the same order as one wave per item.
-// Why: a wave per item with a deep ring keeps ~1000 item streams with ~28 KB
-// in flight each (the HBM side's preference), but at one wave per
-// SIMD it cannot hide an exact entropy (0.56 of HBM with every item exact);
-// a pair keeps ~1000 streams at two waves per SIMD, and an exact entropy costs
-// each wave half the logs.  Both waves run the same top-q (identical keys);
-// wave 1's copy is dropped before the block merge.
-template <int DT, int UNR, int NB>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_stream_wide_pair(
-    WideArgs a, PwPlan pl, StreamArgs sa, int q, Cand* __restrict__ wc) {
-    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
-    CE_DASSERT((int)gridDim.x <= sa.nlists && q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
-    __shared__ WaveListsT<2> sm;
-    __shared__ float xs[2][3];  // per wave: partial f32 row sum, special flag, partial approximate entropy
-    extern __shared__ __attribute__((aligned(16))) double wsm[];
-    constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
-    const int h = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ldr = wide_lds_doubles(a.C);
-    double* rowA = wsm;
-    double* rowB = wsm + ldr;
-    const int64_t W = gridDim.x;  // item streams
-    const int64_t lo0 = blockIdx.x, stride = W;
-    const int64_t cnt = a.N > lo0 ? (a.N - lo0 + W - 1) / W : 0;
-    RegTopQ tq;
-    tq.init(q);
-#if CE_WIDE_PREFILTER
-    if (sa.extra) {  // a chunked job's running list: its q-th entry is an exact floor
-        const Cand e = sa.extra[q - 1];
-        if (e.idx >= 0 && e.key != 0) tq.init(q, e.key, e.idx);
-    }
-#endif
-    const char* base = static_cast<const char*>(a.p);
-    const int64_t sNb = a.sN * EB, sMb = a.sM * EB;
-    const int K = a.C / CPC;
-    const int ch = h * 64 + lane;  // this lane's chunk
-    const bool own = ch < K;
-    const uint32_t off[1] = {16u * (uint32_t)(own ? ch : K - 1)};
-    const int NBM = a.M / UNR;
-    double acc[CPC];
-#pragma unroll
-    for (int e = 0; e < CPC; ++e) acc[e] = 0.0;
-    uint64_t mykey = 0;
-    int64_t myidx = 0;
-    int64_t ii = 0, ci = 0;
-    int ib = 0, cb = 0;
-    WideBatch<DT, 1, UNR> buf[NB];
-    auto issue = [&](WideBatch<DT, 1, UNR>& X) {
-        X.issue(base + (lo0 + ii * stride) * sNb, ib * UNR, sMb, off);
-        if (++ib == NBM) {
-            ib = 0;
-            ++ii;
-        }
-    };
-    auto consume = [&](const WideBatch<DT, 1, UNR>& X) {
-        X.add(acc);
-        if (++cb == NBM) {  // item ci complete (both waves: the same item)
-            cb = 0;
-            bool skip = false;
-#if CE_WIDE_PREFILTER
-            if (tq.tk != 0) {  // wave-uniform, and the same in both waves (identical lists)
-                float mf[CPC];
-                uint32_t hw = 0;
-                float s = 0.0f;
-#pragma unroll
-                for (int e = 0; e < CPC; ++e) {
-                    const double x = own ? acc[e] : 0.0;
-                    const uint32_t t = (uint32_t)(dbits(x) >> 32);
-                    hw = hw > t ? hw : t;
-                    mf[e] = (float)x;
-                    s += mf[e];
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-                const bool sp_part = __ballot(hw >= 0x7ff00000u) != 0;
-                if (lane == 0) {
-                    xs[h][0] = s;
-                    xs[h][1] = sp_part ? 1.0f : 0.0f;
-                }
-                __syncthreads();
-                const float st = xs[0][0] + xs[1][0];
-                const bool special = xs[0][1] != 0.0f || xs[1][1] != 0.0f || !(st >= 0x1p-100f && st <= 0x1p100f);
-                const float r = __builtin_amdgcn_rcpf(st);
-                float hl = 0.0f;
-#pragma unroll
-                for (int e = 0; e < CPC; ++e) {
-                    const float pc = __builtin_fmaxf(mf[e] * r, 0x1p-100f);
-                    hl = __builtin_fmaf(-pc, __builtin_amdgcn_logf(pc), hl);
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) hl += __shfl_xor(hl, o);
-                if (lane == 0) xs[h][2] = hl;
-                __syncthreads();
-                const float ap = xs[0][2] + xs[1][2];
-                if (!special)
-                    skip = tq.tk == ~0ull ||
-                           (double)ap < key_to_val(tq.tk) * 1.4426950408889634 - 2.0 * kWideApproxErr2;
-            }
-#endif
-            double hx = 0.0;
-            if (!skip) {
-#pragma unroll
-                for (int e = 0; e < CPC; ++e) {
-                    acc[e] = div_members(acc[e], a.dM, a.invM, a.pow2);
-                    if (own) rowA[rp(ch * CPC + e)] = acc[e];
-                }
-                __syncthreads();
-                const double s = wave_row_sum(rowA, pl, nullptr);
-#pragma unroll
-                for (int e = 0; e < CPC; ++e)
-                    if (own) rowB[rp(ch * CPC + e)] = entr(1.0 * acc[e] / s);
-                __syncthreads();
-                hx = wave_row_sum(rowB, pl, nullptr);
-            }
-#pragma unroll
-            for (int e = 0; e < CPC; ++e) acc[e] = 0.0;
-            const int j = (int)(ci & 63);
-            if (lane == j) {
-                mykey = skip ? 0ull : order_key(hx);
-                myidx = lo0 + ci * stride;
-            }
-            if (j == 63 || ci == cnt - 1) {
-                bool ok = lane <= j;
-                if (sa.excl) ok = ok && !excluded(sa.excl, lane <= j ? myidx : lo0 + ci * stride);
-                tq.offer(mykey, myidx + sa.base_idx, ok);
-                mykey = 0;
-            }
-            ++ci;
-        }
-    };
-#pragma unroll
-    for (int b = 0; b < NB - 1; ++b)
-        if (ii < cnt) issue(buf[b]);
-    while (ci < cnt) {
-#pragma unroll
-        for (int s = 0; s < NB; ++s) {
-            if (ii < cnt) issue(buf[(s + NB - 1) % NB]);
-            consume(buf[s]);
-            if (ci >= cnt) break;
-        }
-    }
-    if (h == 1) tq.init(q);  // wave 1 held the same list: merged once
-    block_merge_write<2>(tq, sm, q, wc + (int64_t)blockIdx.x * q, sa.nlists, nullptr, nullptr, 2, sa.ctr != nullptr);
-    if (sa.ctr) fold_merge<2>(sa.ctr, sa.oval, sa.oidx, sa.ocand, q, wc, sm, sa.extra);
 }
 
 template <int DT, int NPL, bool VEC>

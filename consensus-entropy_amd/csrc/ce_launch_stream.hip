@@ -29,19 +29,6 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
 // items (M x C x size bytes) from which the wide stream runs one block per CU
 // with a deep register ring (below)
 constexpr int64_t kWideHeavyBytes = 16384;
-#ifndef CE_WIDE_HEAVY
-#define CE_WIDE_HEAVY 0
-#endif
-// the wave-pair wide stream (k_stream_wide_pair) for rows of 65..128 16-B chunks
-#ifndef CE_WIDE_PAIR
-#define CE_WIDE_PAIR 0
-#endif
-#ifndef CE_WIDE_PAIR_NB
-#define CE_WIDE_PAIR_NB 8
-#endif
-#ifndef CE_WIDE_PAIR_PER_CU
-#define CE_WIDE_PAIR_PER_CU 4
-#endif
 
 bool launch_stream(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                    const uint32_t* excl) {
@@ -128,11 +115,11 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             // member rows per batch: 4 / KCH (>= 1), or 1 when that does not divide M
             constexpr int UNR = KCH >= 4 ? 1 : 4 / KCH;
             const int unr = a.M % UNR == 0 ? UNR : 1;
-            auto go = [&](auto kern, int nb, int per_cu) {
+            auto go = [&](auto kern, int nb, int per_cu, StreamArgs s) {
                 note_kernel("ce::k_stream_wide2<%d, %d, %d, %d>", DT, KCH, unr, nb);
                 const int grid = std::min(resident_grid(kern, lds, G), per_cu * device_cus());
-                stream_grid(sa, grid);
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, sa, q, w.c);
+                stream_grid(s, grid);
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, wa, pl, s, q, w.c);
             };
             // A chunked job's chunks after the first (a running list seeds the
             // prefilter's floor, so nearly every item skips its exact entropy)
@@ -146,49 +133,49 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             // 0.813-0.817, a 12-batch ring spills).  Only 4 waves per CU cannot
             // hide exact entropies, though: with every item exact (the build
             // without the prefilter) the same grid reads 0.56 against 0.78, so the
-            // first chunk and single selections keep the occupancy grid.
-#if CE_WIDE_PAIR
-            // a pair of waves per item (k_stream_wide_pair): rows of 65..128 16-B chunks
-            if constexpr (KCH == 2) {
-                const int K = a.C / ChunkT<DT>::CPC;
-                if (R >= kWideHeavyBytes && K > 64 && K <= 128 && sa.excl == nullptr) {
-                    const size_t plds = 2 * (size_t)wide_lds_doubles(a.C) * sizeof(double);
-                    auto pgo = [&](auto kern, int unr_) {
-                        note_kernel("ce::k_stream_wide_pair<%d, %d, %d>", DT, unr_, CE_WIDE_PAIR_NB);
-                        int per_cu = 0;
-                        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 128, plds) != hipSuccess ||
-                            per_cu < 1)
-                            per_cu = 1;
-                        (void)hipGetLastError();
-                        per_cu = std::min(per_cu, CE_WIDE_PAIR_PER_CU);
-                        const int grid = std::min(per_cu * device_cus(), G);
-                        sa.nlists = G;
-                        hipLaunchKernelGGL(kern, dim3(grid), dim3(128), plds, st, wa, pl, sa, q, w.c);
-                    };
-                    if (a.M % 4 == 0) pgo(k_stream_wide_pair<DT, 4, CE_WIDE_PAIR_NB>, 4);
-                    else pgo(k_stream_wide_pair<DT, 1, CE_WIDE_PAIR_NB>, 1);
-                    return;
-                }
-            }
-#endif
-            bool heavy = false;
-            if constexpr (KCH <= 2) {  // (wider lanes: 8 batches would spill)
-#if CE_WIDE_HEAVY == 1  // A/B: every long pool (>= 256 items per wave) on the deep-ring grid
-                heavy = R >= kWideHeavyBytes && a.N >= 1024 * (int64_t)device_cus() && CE_WIDE_PREFILTER;
-#else
-                heavy = R >= kWideHeavyBytes && fold != nullptr && fold->extra != nullptr && CE_WIDE_PREFILTER;
-#endif
-            }
-            if (heavy) {
+            // first chunk and single selections keep the occupancy grid, and a
+            // seeded chunk runs it only when the grid vote (k_wide_vote) finds at
+            // most 1/16 of its samples beating the running floor: a chunk of
+            // rising entropies (every item exact) read 0.51 on the deep grid,
+            // 0.79-0.82 on the occupancy grid (profiles/r06_c5_vote.json).  A
+            // wave PAIR per item on the deep grid (two waves per SIMD, each half
+            // the classes) was measured and dropped: 0.61 on that pool, 0.77-0.79
+            // where the deep grid reads 0.86-0.89 (the same file).
+            bool seeded = false;  // a chunked job's chunk after the first, heavy items
+            if constexpr (KCH <= 2)   // (wider lanes: 8 batches would spill)
+                seeded = R >= kWideHeavyBytes && fold != nullptr && fold->extra != nullptr &&
+                         fold->vote != nullptr && CE_WIDE_PREFILTER;
+            if (seeded) {
                 if constexpr (KCH <= 2) {
-                    if (unr == UNR) go(k_stream_wide2<DT, KCH, UNR, 8>, 8, 1);
-                    else go(k_stream_wide2<DT, KCH, 1, 8>, 8, 1);
+                    // the grid vote (k_wide_vote, ce_kernels.hpp), then both grids:
+                    // the one the vote does not pick exits at its first instruction
+                    const int64_t ns = std::min<int64_t>(a.N, kWideVoteSamples);
+                    if (hipMemsetAsync(fold->vote, 0, sizeof(uint32_t), st) != hipSuccess) {
+                        rc_excl = CE_ELAUNCH;
+                        return;
+                    }
+                    auto vk = unr == UNR ? k_wide_vote<DT, KCH, UNR> : k_wide_vote<DT, KCH, 1>;
+                    hipLaunchKernelGGL(vk, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, st, wa, fold->extra, q,
+                                       fold->vote);
+                    StreamArgs sh = sa, so = sa;
+                    sh.vote = so.vote = fold->vote;
+                    sh.vote_heavy = 1;
+                    so.vote_heavy = 0;
+                    if (unr == UNR) {
+                        go(k_stream_wide2<DT, KCH, UNR, 8>, 8, 1, sh);
+                        go(k_stream_wide2<DT, KCH, UNR, 2>, 2, 1 << 20, so);
+                    } else {
+                        go(k_stream_wide2<DT, KCH, 1, 8>, 8, 1, sh);
+                        go(k_stream_wide2<DT, KCH, 1, 2>, 2, 1 << 20, so);
+                    }
+                    note_kernel("ce::k_stream_wide2<%d, %d, %d, 8>|ce::k_stream_wide2<%d, %d, %d, 2>", DT, KCH, unr,
+                                DT, KCH, unr);
                 }
             } else {
                 // a 2-batch register ring at the occupancy grid (3 and 4 measured:
                 // 72.8 / 71.9 % vs 72.6 % at C5 in round 2)
-                if (unr == UNR) go(k_stream_wide2<DT, KCH, UNR, 2>, 2, 1 << 20);
-                else go(k_stream_wide2<DT, KCH, 1, 2>, 2, 1 << 20);
+                if (unr == UNR) go(k_stream_wide2<DT, KCH, UNR, 2>, 2, 1 << 20, sa);
+                else go(k_stream_wide2<DT, KCH, 1, 2>, 2, 1 << 20, sa);
             }
         } else {  // strided / unaligned rows: the unpipelined wave-per-item kernel
             if (sa.excl) {  // k_stream_wide takes no bitmap

@@ -49,8 +49,18 @@
 namespace ce {
 
 constexpr int kXgbTile = 64;      // frames per block
-constexpr int kXgbPad = 65;       // LDS column stride (floats)
+// LDS tile: feature-major columns of 64 floats, frame r of feature f at f*64 +
+// (r ^ (f & 63)) -- the XOR swizzle keeps the staging writes (consecutive
+// features of one frame) conflict-free, and a column read by 64 lanes is a
+// permutation of one column (conflict-free too).  Byte address of (f, lane):
+// fbase(f) ^ 4*lane with fbase(f) = 256 f + 4 (f & 63).
+constexpr int kXgbCol = 64;
+__device__ __forceinline__ uint32_t xs_fbase(uint32_t f) { return f * 256u + ((f & 63u) << 2); }
+__device__ __forceinline__ float xs_at(const float* xs, uint32_t fbase, uint32_t lane4) {
+    return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(xs) + (fbase ^ lane4));
+}
 constexpr int kXgbMaxDepth = 10;  // packed depth limit (2^10 leaves per tree)
+constexpr int kXgbLaneDepth = 5;  // lane-table walk: 2^(d+1) - 1 entries fit one wave
 constexpr int kXgbMaxFeat = 512;
 constexpr int kXgbMaxGroups = 8;
 // level 1 of every tree from the wave-uniform node pair {1, 2} (one scalar
@@ -111,9 +121,10 @@ struct XgbArgs {
     int64_t ldo;
 };
 
-// Stage frames [f0, f0 + 64) of X as float32 into LDS, feature-major [D][65]
-// (consecutive threads take consecutive features of a row: conflict-free
-// writes); rows past the end repeat the last frame.  8 loads in flight.
+// Stage frames [f0, f0 + 64) of X as float32 into LDS, feature-major [D][64]
+// swizzled (kXgbCol; consecutive threads take consecutive features of a row:
+// conflict-free writes); rows past the end repeat the last frame.  8 loads in
+// flight.
 // Returns whether this thread staged a NaN (missing value).
 template <int XDT>
 __device__ __forceinline__ bool stage_tile(const void* X, int64_t F, int D, int64_t ld, int64_t f0, int nf,
@@ -133,7 +144,7 @@ __device__ __forceinline__ bool stage_tile(const void* X, int64_t F, int D, int6
                 v[u] = (float)static_cast<const double*>(X)[row * ld + f];
             else
                 v[u] = static_cast<const float*>(X)[row * ld + f];
-            dst[u] = e < total ? f * kXgbPad + r : -1;
+            dst[u] = e < total ? f * kXgbCol + (r ^ (f & 63)) : -1;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -194,7 +205,7 @@ struct WalkForest {
     template <bool MISS>
     static __device__ __forceinline__ bool go_right(uint2 nd, const float* xs, int D, int lane) {
         const int ft = min((int)(nd.x & 0x7fffffffu), D - 1);  // packer checks < D
-        const float x = xs[ft * kXgbPad + lane];
+        const float x = xs_at(xs, xs_fbase((uint32_t)ft), 4u * (uint32_t)lane);
         const float th = __uint_as_float(nd.y);
         if constexpr (MISS)  // missing -> default child; else fvalue < split_cond ? left : right
             return __builtin_isnan(x) ? (nd.x >> 31) == 0u : !(x < th);
@@ -265,6 +276,105 @@ struct WalkForest {
         CE_DASSERT(t >= 0 && t < goff_end && li >= 0 && li <= NI);
         return leaves[(int64_t)t * (NI + 1) + li];
     }
+    // trees [t0, min(t0 + 8, t1)): leaf indices, and (VALS) their leaf values
+    template <bool MISS, bool VALS>
+    __device__ __forceinline__ void walk8(const float* xs, int D, int t0, int t1, int lane, int (&li)[8],
+                                          float (&v)[8]) const {
+        leafidx8<MISS>(xs, D, t0, t1, lane, li);
+        if constexpr (VALS) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = value(t0 + j < t1 ? t0 + j : t1 - 1, li[j]);
+        }
+    }
+};
+
+// Lane-table walk (perfect trees of depth <= 5: 2^d - 1 nodes + 2^d leaves <=
+// 63 entries, the reference's XGBClassifier(max_depth=5)).  A tree's table is
+// read with two COALESCED loads -- lane i holds entry i: node i (i < NI) or
+// leaf i - NI (NI <= i <= 2 NI) -- and each level fetches every lane's current
+// node from the table with ds_bpermute (the LDS crossbar: no memory access,
+// no address chain through L2): 2 loads per tree instead of 1 scalar pair + 3
+// per-lane gathers + 1 leaf gather on the texture path the walk was bound by
+// (TA 74-79 % busy).  The node's feature is kept as its LDS
+// column base (xs_fbase, the clamp to D - 1 done once), so a level is two
+// bpermutes, one XOR, one ds_read, one compare and the index update.  The
+// root (entry 0) is read with v_readlane: wave-uniform.
+struct LaneForest {
+    const uint2* nodes;   // [T][NI]
+    const float* leaves;  // [T][NI + 1]
+    const int32_t* goff;
+    int depth, NI;
+    int goff_end;
+
+    // this lane's table entry of tree t: fx = xs_fbase(feature) (| default_left << 31
+    // when MISS), ty = the split condition's bits; at a leaf entry fx = 0, ty = the
+    // leaf value's bits; past the table both 0
+    template <bool MISS>
+    __device__ __forceinline__ void entry(int t, int D, int lane, uint32_t& fx, uint32_t& ty) const {
+        fx = 0u;
+        ty = 0u;
+        if (lane < NI) {
+            const uint2 nd = nodes[(int64_t)t * NI + lane];
+            const uint32_t ft = min(nd.x & 0x7fffffffu, (uint32_t)(D - 1));  // packer checks < D
+            fx = xs_fbase(ft) | (MISS ? (nd.x & 0x80000000u) : 0u);
+            ty = nd.y;
+        } else if (lane <= 2 * NI) {
+            ty = __float_as_uint(leaves[(int64_t)t * (NI + 1) + (lane - NI)]);
+        }
+    }
+    template <bool MISS>
+    static __device__ __forceinline__ bool right(uint32_t fx, uint32_t th, const float* xs, uint32_t lane4) {
+        const float x = xs_at(xs, MISS ? (fx & 0x7fffffffu) : fx, lane4);
+        if constexpr (MISS)  // missing -> default child; else fvalue < split_cond ? left : right
+            return __builtin_isnan(x) ? (fx >> 31) == 0u : !(x < __uint_as_float(th));
+        else
+            return !(x < __uint_as_float(th));
+    }
+    static __device__ __forceinline__ uint32_t bperm(int idx4, uint32_t v) {
+        return (uint32_t)__builtin_amdgcn_ds_bpermute(idx4, (int)v);
+    }
+    template <bool MISS, bool VALS>
+    __device__ __forceinline__ void walk8(const float* xs, int D, int t0, int t1, int lane, int (&li)[8],
+                                          float (&v)[8]) const {
+        uint32_t fx[8], ty[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) entry<MISS>(t0 + j < t1 ? t0 + j : t1 - 1, D, lane, fx[j], ty[j]);
+        const uint32_t lane4 = 4u * (uint32_t)lane;
+        int idx4[8];  // 4 x the lane's node index (a ds_bpermute byte address); children 2 idx4 + 4 / + 8
+#pragma unroll
+        for (int j = 0; j < 8; ++j) idx4[j] = 0;
+        if (depth >= 1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)fx[j], 0);
+                const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)ty[j], 0);
+                idx4[j] = right<MISS>(f0, h0, xs, lane4) ? 8 : 4;
+            }
+        }
+        for (int lev = 1; lev < depth; ++lev) {
+            uint32_t f[8], h[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                f[j] = bperm(idx4[j], fx[j]);
+                h[j] = bperm(idx4[j], ty[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) idx4[j] = 2 * idx4[j] + (right<MISS>(f[j], h[j], xs, lane4) ? 8 : 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            li[j] = (idx4[j] >> 2) - NI;
+            CE_DASSERT(li[j] >= 0 && li[j] <= NI);
+        }
+        if constexpr (VALS) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = __uint_as_float(bperm(idx4[j], ty[j]));
+        }
+    }
+    __device__ __forceinline__ float value(int t, int li) const {
+        CE_DASSERT(t >= 0 && t < goff_end && li >= 0 && li <= NI);
+        return leaves[(int64_t)t * (NI + 1) + li];
+    }
 };
 
 // ---- one block per 64-frame tile: G x S waves ------------------------------
@@ -292,10 +402,8 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
         int npend = 0;
         for (int k = k0; k < head_end; k += 8) {
             int li[8];
-            fl.template leafidx8<MISS>(xs, a.D, k, head_end, lane, li);
             float v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = fl.value(k + j < head_end ? k + j : head_end - 1, li[j]);
+            fl.template walk8<MISS, true>(xs, a.D, k, head_end, lane, li, v);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 if (j < npend) m += pend[j];
@@ -314,7 +422,8 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
         for (int b = 0; b < kXgbChunk / 8; ++b) {
             if (b * 8 < cnt) {
                 int li[8];
-                fl.template leafidx8<MISS>(xs, a.D, lo + b * 8, hi, lane, li);
+                float v[8];
+                fl.template walk8<MISS, false>(xs, a.D, lo + b * 8, hi, lane, li, v);
 #pragma unroll
                 for (int j = 0; j < 8; j += 2) packed[b * 4 + j / 2] = (uint32_t)li[j] | ((uint32_t)li[j + 1] << 16);
             }
@@ -347,8 +456,8 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
 template <int XDT, int ODT, class L>
 __device__ __forceinline__ void xgb_tile(const XgbArgs& a, const L& fl) {
     extern __shared__ float xsm[];
-    float* xs = xsm;                  // [D][kXgbPad]
-    float* mg = xsm + a.D * kXgbPad;  // [G][64] margins
+    float* xs = xsm;                  // [D][kXgbCol] swizzled
+    float* mg = xsm + a.D * kXgbCol;  // [G][64] margins
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = w / a.S, s = w - g * a.S;
@@ -362,16 +471,22 @@ __device__ __forceinline__ void xgb_tile(const XgbArgs& a, const L& fl) {
     transform_store<ODT>(mg, a.G, a.C, f0, nf, a.out, a.ldo);
 }
 
-template <int XDT, int ODT>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_xgb_walk(XgbArgs a, const uint2* __restrict__ nodes,
-                                                   const float* __restrict__ leaves, const int32_t* __restrict__ goff,
-                                                   int depth) {
+// LANES: the lane-table walk (depth <= 5), else the perfect-tree gather walk
+template <int XDT, int ODT, bool LANES>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_xgb_walk(
+    XgbArgs a, const uint2* __restrict__ nodes, const float* __restrict__ leaves, const int32_t* __restrict__ goff,
+    int depth) {
 #ifdef CE_DEBUG
     const int T = goff[a.G];
 #else
     const int T = 0;
 #endif
-    xgb_tile<XDT, ODT>(a, WalkForest{nodes, leaves, goff, depth, (1 << depth) - 1, T});
+    if constexpr (LANES) {
+        CE_DASSERT(depth <= kXgbLaneDepth);
+        xgb_tile<XDT, ODT>(a, LaneForest{nodes, leaves, goff, depth, (1 << depth) - 1, T});
+    } else {
+        xgb_tile<XDT, ODT>(a, WalkForest{nodes, leaves, goff, depth, (1 << depth) - 1, T});
+    }
 }
 
 __global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
@@ -385,7 +500,7 @@ __global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict
 using namespace ce;
 
 extern "C" size_t ce_xgb_lds_bytes(int32_t D, int32_t G) {
-    return (size_t)D * kXgbPad * sizeof(float) + (size_t)std::max(G, 1) * 64 * sizeof(float);
+    return (size_t)D * kXgbCol * sizeof(float) + (size_t)std::max(G, 1) * 64 * sizeof(float);
 }
 
 // waves per group: fill a 16-wave block
@@ -430,8 +545,10 @@ extern "C" int ce_xgb_predict_proba(const void* X, ce_dtype x_dt, int64_t F, int
     const int S = xgb_splits(G);
     const XgbArgs a{X, F, D, ld, G, C, S, base_margin, out, ld_out};
     xgb_dispatch(x_dt, out_dt, [&](auto xd, auto od) {
-        xgb_launch(k_xgb_walk<decltype(xd)::value, decltype(od)::value>, F, ce_xgb_lds_bytes(D, G), 64 * G * S,
-                   stream, a, reinterpret_cast<const uint2*>(nodes), leaves, group_offsets, depth);
+        constexpr int XD = decltype(xd)::value, OD = decltype(od)::value;
+        const auto kern = depth <= kXgbLaneDepth ? k_xgb_walk<XD, OD, true> : k_xgb_walk<XD, OD, false>;
+        xgb_launch(kern, F, ce_xgb_lds_bytes(D, G), 64 * G * S, stream, a, reinterpret_cast<const uint2*>(nodes),
+                   leaves, group_offsets, depth);
     });
     return check_launch("ce_xgb_predict_proba");
 }

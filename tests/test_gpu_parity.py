@@ -1216,6 +1216,41 @@ def test_chunked_pool_vs_oracle(ce, C, dt, N, chunk):
     assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
 
 
+@pytest.mark.parametrize("order", ["rising", "falling", "mixed"])
+def test_chunked_grid_vote_orders(ce, order):
+    """The seeded chunks' device-side grid vote (k_wide_vote: the deep-ring
+    grid when at most 1/16 of 1024 sampled items beat the running list's q-th
+    entry, else the occupancy grid; both are launched, one exits): chunks whose
+    entropies rise (every item beats the floor -> occupancy grid), fall (every
+    item skips -> deep grid) and alternate, 32 x 1000 bf16 (64 KB items), with
+    exact ties on the boundaries -- the job equals the oracle either way."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng({"rising": 61, "falling": 62, "mixed": 63}[order])
+    N, M, C, chunk = 7_200, 32, 1000, 1_200
+    P = synth(rng, N, M, C, np.float32)
+    # K_i classes near 1.0 and the rest near 2^-10: entropy grows with K_i
+    k = 1 + (np.arange(N) * 999) // N
+    if order == "falling":
+        k = k[::-1]
+    elif order == "mixed":
+        k = np.concatenate([k[lo:lo + chunk][::(-1) ** (lo // chunk)] for lo in range(0, N, chunk)])
+    base = np.where(np.arange(C)[None, :] < k[:, None], 1.0, 2.0 ** -10)
+    P = (base[:, None, :] * (1.0 + 0.05 * P)).astype(np.float32)
+    for b in range(chunk, N, chunk):
+        P[b - 1:b + 1] = P[b - 2]  # identical rows across each boundary: the earlier position wins
+    host = _bf16_bits(P)
+    Pd = dev(host.view(np.int16)).view(torch.bfloat16)
+    ent_o = O.oracle_committee_entropy(host, "NMC")
+    for q in (1, 10, 64):
+        _, idx_o = O.oracle_topq(ent_o, q)
+        job = ce.ops.MCChunkJob(q, "NMC")
+        for lo in range(0, N, chunk):
+            job.add(Pd[lo:lo + chunk])
+        _, idx = job.result()
+        assert np.array_equal(idx_np(idx), idx_o), (order, q)
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 def test_wide_prefilter_specials(ce, dt):
     """The wide stream's approximate prefilter (ce_wide.hpp: items whose f32

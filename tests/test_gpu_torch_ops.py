@@ -268,8 +268,10 @@ def test_wide_chunks_grid_rule(tops):
     """The wide stream's grid (csrc/ce_launch_stream.hip): a chunked job's first
     chunk and single selections run the occupancy grid with a 2-batch ring;
     the chunks after the first (prefilter seeded by the running list) with
-    >= 16 KiB items run one block per CU with an 8-batch ring -- and the job
-    selects what one launch over the whole pool selects."""
+    >= 16 KiB items launch the grid vote and BOTH grids -- one block per CU
+    with an 8-batch ring, and the occupancy grid; the one the vote does not
+    pick exits at once (ce_last_kernel() names both) -- and the job selects
+    what one launch over the whole pool selects."""
     import ce_amd
     import ce_amd.ops as ops
 
@@ -280,7 +282,7 @@ def test_wide_chunks_grid_rule(tops):
     job.add(P[:2000])
     assert lib.ce_last_kernel().decode() == "ce::k_stream_wide2<2, 2, 2, 2>"
     job.add(P[2000:4000])
-    assert lib.ce_last_kernel().decode() == "ce::k_stream_wide2<2, 2, 2, 8>"
+    assert lib.ce_last_kernel().decode() == "ce::k_stream_wide2<2, 2, 2, 8>|ce::k_stream_wide2<2, 2, 2, 2>"
     job.add(P[4000:])
     v, i = job.result()
     v1, i1 = ops.select_mc(P, 10, "NMC")
