@@ -522,9 +522,17 @@ def xgb_predict_proba(X, forest, out=None, out_dtype=torch.float32):
     if out.dim() != 2 or out.shape[0] != F or out.shape[1] < C or out.stride(1) != 1 or out.dtype not in _DT:
         raise ValueError(f"out must be a float [{F}, >={C}] tensor with unit column stride")
     nodes, leaves, goff, depth = forest.device_arrays(X.device)
-    call("ce_xgb_predict_proba", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(nodes), _p(leaves), _p(goff), G, depth,
-         float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0), _stream(X.device))
+    if depth <= LANE_TABLE_DEPTH:  # the reference's max_depth=5: prebuilt per-tree lane tables
+        table = forest.lane_table(X.device, D)
+        call("ce_xgb_predict_proba_lanes", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(table), _p(goff), G, depth,
+             float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0), _stream(X.device))
+    else:
+        call("ce_xgb_predict_proba", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(nodes), _p(leaves), _p(goff), G,
+             depth, float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0), _stream(X.device))
     return out
+
+
+LANE_TABLE_DEPTH = 5  # csrc/ce_xgb.hip kXgbLaneDepth: 2^(d+1) heap entries fit one wave
 
 
 def _check_q(q):

@@ -183,6 +183,25 @@ class XgbForest:
     def max_feature(self):
         return max((int(tr["split"][tr["left"] != -1].max(initial=-1)) for tr in self.trees), default=-1)
 
+    def lane_table(self, device, D):
+        """The prebuilt per-tree lane tables of ce_xgb_predict_proba_lanes (depth
+        <= 5): int32 [T, 64, 2] on ``device`` for X with D columns, built once on
+        the device by ce_xgb_lane_table and cached per (device, D)."""
+        import torch
+
+        from . import _lib
+        from .ops import _p, _stream, call
+
+        key = (torch.device(device), int(D))
+        if key not in self._dev:
+            nodes, leaves, _, d = self.device_arrays(device)
+            T = len(self.trees)
+            table = torch.empty((T, 64, 2), dtype=torch.int32, device=key[0])
+            _lib.load()
+            call("ce_xgb_lane_table", _p(nodes), _p(leaves), T, d, int(D), _p(table), _stream(key[0]))
+            self._dev[key] = table
+        return self._dev[key]
+
     def device_arrays(self, device):
         """The packed arrays as device tensors (cached per device)."""
         import torch

@@ -122,36 +122,48 @@ struct XgbArgs {
 };
 
 // Stage frames [f0, f0 + 64) of X as float32 into LDS, feature-major [D][64]
-// swizzled (kXgbCol; consecutive threads take consecutive features of a row:
-// conflict-free writes); rows past the end repeat the last frame.  8 loads in
-// flight.
+// swizzled (kXgbCol): wave w takes rows w, w + W, ..., its lanes consecutive
+// features of a row (coalesced loads; conflict-free writes: bank r ^ lane), 2
+// rows x 8 feature chunks per lane in flight; rows past the end repeat the
+// last frame.  No index division: the round-5 loop's e / D cost ~40 VALU per
+// element -- a third of the kernel's VALU (PMC r06).
 // Returns whether this thread staged a NaN (missing value).
-template <int XDT>
+template <int XDT, int KF = kXgbMaxFeat / 64>  // KF: 64-feature chunks per row, >= ceil(D / 64)
 __device__ __forceinline__ bool stage_tile(const void* X, int64_t F, int D, int64_t ld, int64_t f0, int nf,
                                            float* xs) {
-    const int total = kXgbTile * D;
+    (void)F;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, W = blockDim.x >> 6;
     bool has_nan = false;
-    for (int e0 = threadIdx.x; e0 < total; e0 += blockDim.x * 8) {
-        float v[8];
-        int dst[8];
+    for (int r0 = w; r0 < kXgbTile; r0 += 2 * W) {  // wave-uniform
+        // every load unconditional (clamped row / feature): a load under a branch
+        // gets its own s_waitcnt vmcnt(0), serialising the 16 round trips
+        typename std::conditional<XDT == CE_F64, double, float>::type v[2][KF];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = e0 + u * blockDim.x;
-            const int ec = e < total ? e : total - 1;
-            const int r = ec / D, f = ec - r * D;
-            const int64_t row = f0 + (r < nf ? r : nf - 1);
-            if constexpr (XDT == CE_F64)
-                v[u] = (float)static_cast<const double*>(X)[row * ld + f];
-            else
-                v[u] = static_cast<const float*>(X)[row * ld + f];
-            dst[u] = e < total ? f * kXgbCol + (r ^ (f & 63)) : -1;
+        for (int h = 0; h < 2; ++h) {
+            const int r = min(r0 + h * W, kXgbTile - 1);
+            const int64_t row = f0 + min(r, nf - 1);
+#pragma unroll
+            for (int k = 0; k < KF; ++k) {
+                const int f = min(lane + 64 * k, D - 1);
+                if constexpr (XDT == CE_F64)
+                    v[h][k] = static_cast<const double*>(X)[row * ld + f];
+                else
+                    v[h][k] = static_cast<const float*>(X)[row * ld + f];
+            }
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (dst[u] >= 0) {
-                xs[dst[u]] = v[u];
-                has_nan |= __builtin_isnan(v[u]);
+        for (int h = 0; h < 2; ++h) {
+            const int r = r0 + h * W;
+#pragma unroll
+            for (int k = 0; k < KF; ++k) {
+                const int f = lane + 64 * k;
+                if (f < D && r < kXgbTile) {
+                    const float x = (float)v[h][k];
+                    xs[f * kXgbCol + (r ^ lane)] = x;  // (f & 63) == lane
+                    has_nan |= __builtin_isnan(x);
+                }
             }
+        }
     }
     return has_nan;
 }
@@ -377,6 +389,97 @@ struct LaneForest {
     }
 };
 
+// Prebuilt lane tables (ce_xgb_lane_table; depth <= 5): tree t's 64 entries
+// [t][64] x {fx, ty} in a 1-based heap -- lane j in [1, 2^d) holds node j - 1
+// as {xs_fbase(min(feature, D - 1)) | default_left << 31, split_cond bits},
+// lane 2^d + k leaf k as {0, leaf bits}, lane 0 and the rest {0, 0} -- so one
+// coalesced dwordx2 load with a scalar base is a tree's whole table (no
+// per-lane branches or feature arithmetic), the root comes from a scalar load,
+// and a level is child = 2 j + right.  VALU per tree was the limiter of the
+// on-the-fly tables (PMC r06: VALU 72 % busy, 80 VALU per tree and wave).
+struct LaneTableForest {
+    const uint2* table;   // [T][64]
+    const int32_t* goff;
+    int depth, NI;
+    int goff_end;
+
+    // fx carries default_left in bit 31 either way (masked in the address: one v_bitop3)
+    template <bool MISS>
+    static __device__ __forceinline__ bool right(uint32_t fx, uint32_t th, const float* xs, uint32_t lane4) {
+        const float x = xs_at(xs, fx & 0x7fffffffu, lane4);
+        // missing -> the default child, else fvalue < split_cond ? left : right; a
+        // NaN fails the compare (right), so flip exactly the NaN lanes whose default
+        // is left: three compares and two mask ops
+        const bool r = !(x < __uint_as_float(th));
+        if constexpr (MISS)
+            return r != (__builtin_isnan(x) && (int32_t)fx < 0);
+        else
+            return r;
+    }
+    // 4 trees at a time (two rounds per batch of 8): 4 independent chains per
+    // lane keep every level's 8 bpermutes in flight within the 64-VGPR budget of
+    // 8 waves per SIMD (8 chains forced the compiler to serialize the split
+    // conditions' bpermutes behind lgkmcnt(0)); the second round's tables are
+    // loaded with the first's.
+    template <bool MISS, bool VALS>
+    __device__ __forceinline__ void walk8(const float* xs, int D, int t0, int t1, int lane, int (&li)[8],
+                                          float (&v)[8]) const {
+        (void)D;
+        uint2 e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = table[(int64_t)(t0 + j < t1 ? t0 + j : t1 - 1) * 64 + lane];
+        const uint32_t lane4 = 4u * (uint32_t)lane;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            int h[4];  // the lane's heap index x 4 (a ds_bpermute byte address): root 4, children 2 h + 4 b
+#pragma unroll
+            for (int j = 0; j < 4; ++j) h[j] = 4;
+            // entries 0..3 of each tree (root 1, level-1 pair 2 / 3): 32 wave-uniform
+            // bytes, scalar loads issued together before the first use (one wait)
+            uint4 q0[4], q1[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int t = t0 + 4 * g + j < t1 ? t0 + 4 * g + j : t1 - 1;
+                const uint4* p = reinterpret_cast<const uint4*>(table + (int64_t)t * 64);
+                q0[j] = p[0];
+                q1[j] = p[1];
+            }
+            if (depth >= 1) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) h[j] = right<MISS>(q0[j].z, q0[j].w, xs, lane4) ? 12 : 8;
+            }
+            if (depth >= 2) {  // level 1 from the pair {2, 3} and a select
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool rt = h[j] == 12;
+                    const uint32_t f = rt ? q1[j].z : q1[j].x, th = rt ? q1[j].w : q1[j].y;
+                    h[j] = 2 * h[j] + (right<MISS>(f, th, xs, lane4) ? 4 : 0);
+                }
+            }
+            for (int lev = 2; lev < depth; ++lev) {
+                uint32_t f[4], th[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    f[j] = LaneForest::bperm(h[j], e[4 * g + j].x);
+                    th[j] = LaneForest::bperm(h[j], e[4 * g + j].y);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) h[j] = 2 * h[j] + (right<MISS>(f[j], th[j], xs, lane4) ? 4 : 0);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                li[4 * g + j] = (h[j] >> 2) - (NI + 1);
+                CE_DASSERT(li[4 * g + j] >= 0 && li[4 * g + j] <= NI);
+                if constexpr (VALS) v[4 * g + j] = __uint_as_float(LaneForest::bperm(h[j], e[4 * g + j].y));
+            }
+        }
+    }
+    __device__ __forceinline__ float value(int t, int li) const {
+        CE_DASSERT(t >= 0 && t < goff_end && li >= 0 && li <= NI);
+        return __uint_as_float(table[(int64_t)t * 64 + NI + 1 + li].y);
+    }
+};
+
 // ---- one block per 64-frame tile: G x S waves ------------------------------
 // Wave (g, s) takes a contiguous run of group g's trees: s = 0 the head, its
 // leaves added straight into the margin (a batch's leaf loads are added after
@@ -429,42 +532,48 @@ __device__ __forceinline__ void split_margins(const XgbArgs& a, const L& fl, con
             }
         }
     }
+    // the tail wave's leaf values, all loaded before the ordered phases (one
+    // latency, not one per phase: the phases are a chain of S - 1 hand-offs);
+    // slots past cnt re-read the clamped last (tree, leaf) -- in bounds, not added
+    float tv[kXgbChunk];
+#pragma unroll
+    for (int i = 0; i < kXgbChunk; ++i)
+        tv[i] = (s > 0 && i < cnt) ? fl.value(lo + i, (packed[i / 2] >> (16 * (i & 1))) & 0xffffu) : 0.0f;
     for (int ph = 0; ph < S; ++ph) {
         if (s == ph && s > 0) {
             m = mg[g * 64 + lane];
 #pragma unroll
-            for (int b = 0; b < kXgbChunk / 8; ++b) {
-                if (b * 8 >= cnt) break;  // wave-uniform; never load past the wave's trees
-                float v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    // slots past cnt hold the leaf of the batch's clamped last tree (leafidx8):
-                    // re-read that (tree, leaf) -- in bounds, not added
-                    const int i = b * 8 + j;
-                    v[j] = fl.value(lo + min(i, cnt - 1), (packed[i / 2] >> (16 * (i & 1))) & 0xffffu);
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (b * 8 + j < cnt) m += v[j];
-            }
+            for (int i = 0; i < kXgbChunk; ++i)
+                if (i < cnt) m += tv[i];
         }
         if (s == ph) mg[g * 64 + lane] = m;
         __syncthreads();
     }
 }
 
-template <int XDT, int ODT, class L>
+template <int XDT, int ODT, class L, int KF = kXgbMaxFeat / 64>
 __device__ __forceinline__ void xgb_tile(const XgbArgs& a, const L& fl) {
     extern __shared__ float xsm[];
     float* xs = xsm;                  // [D][kXgbCol] swizzled
     float* mg = xsm + a.D * kXgbCol;  // [G][64] margins
+    uint32_t* nanw = reinterpret_cast<uint32_t*>(mg + a.G * 64);  // [waves] the tile's missing-value votes
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = w / a.S, s = w - g * a.S;
     const int64_t f0 = (int64_t)blockIdx.x * kXgbTile;
     const int nf = (int)min<int64_t>(kXgbTile, a.F - f0);
-    const bool has_nan = stage_tile<XDT>(a.X, a.F, a.D, a.ld, f0, nf, xs);
-    if (__syncthreads_or(has_nan))
+    const bool has_nan = stage_tile<XDT, KF>(a.X, a.F, a.D, a.ld, f0, nf, xs);
+    // the block's "any NaN" vote through the dynamic LDS (__syncthreads_or keeps
+    // a static LDS word, which puts the tile 256 B off address 0: one more VALU
+    // per node read)
+    {
+        const bool wn = __ballot(has_nan) != 0;
+        if (lane == 0) nanw[w] = wn ? 1u : 0u;
+    }
+    __syncthreads();
+    bool any_nan = false;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) any_nan |= nanw[k] != 0u;
+    if (any_nan)
         split_margins<L, true>(a, fl, xs, mg, g, s, lane);
     else
         split_margins<L, false>(a, fl, xs, mg, g, s, lane);
@@ -489,6 +598,37 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     }
 }
 
+// KF: the row's 64-feature chunks the staging loads (>= ceil(D / 64); every load
+// is unconditional, so a smaller KF drops dead loads: D = 260 takes 5 of 8)
+template <int XDT, int ODT, int KF>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_xgb_lanes(
+    XgbArgs a, const uint2* __restrict__ table, const int32_t* __restrict__ goff, int depth) {
+#ifdef CE_DEBUG
+    const int T = goff[a.G];
+#else
+    const int T = 0;
+#endif
+    CE_DASSERT(depth <= kXgbLaneDepth);
+    xgb_tile<XDT, ODT, LaneTableForest, KF>(a, LaneTableForest{table, goff, depth, (1 << depth) - 1, T});
+}
+
+// ce_xgb_lane_table: one wave per tree, lane j writes heap entry j
+__global__ __launch_bounds__(256) void k_xgb_lane_table(const uint2* __restrict__ nodes, const float* __restrict__ leaves,
+                                                        int T, int depth, int D, uint2* __restrict__ table) {
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int j = threadIdx.x & 63, NI = (1 << depth) - 1;
+    if (t >= T) return;
+    uint2 e = make_uint2(0u, 0u);
+    if (j >= 1 && j <= NI) {
+        const uint2 nd = nodes[t * NI + (j - 1)];
+        const uint32_t ft = min(nd.x & 0x7fffffffu, (uint32_t)(D - 1));
+        e = make_uint2(xs_fbase(ft) | (nd.x & 0x80000000u), nd.y);
+    } else if (j >= NI + 1 && j <= 2 * NI + 1) {
+        e = make_uint2(0u, __float_as_uint(leaves[t * (NI + 1) + (j - NI - 1)]));
+    }
+    table[t * 64 + j] = e;
+}
+
 __global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -500,7 +640,7 @@ __global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict
 using namespace ce;
 
 extern "C" size_t ce_xgb_lds_bytes(int32_t D, int32_t G) {
-    return (size_t)D * kXgbCol * sizeof(float) + (size_t)std::max(G, 1) * 64 * sizeof(float);
+    return (size_t)D * kXgbCol * sizeof(float) + (size_t)std::max(G, 1) * 64 * sizeof(float) + 16 * sizeof(uint32_t);
 }
 
 // waves per group: fill a 16-wave block
@@ -551,6 +691,39 @@ extern "C" int ce_xgb_predict_proba(const void* X, ce_dtype x_dt, int64_t F, int
                    leaves, group_offsets, depth);
     });
     return check_launch("ce_xgb_predict_proba");
+}
+
+extern "C" int ce_xgb_lane_table(const uint32_t* nodes, const float* leaves, int32_t T, int32_t depth, int32_t D,
+                                 uint32_t* table, ce_stream_t stream) {
+    if (T < 0 || depth < 0 || depth > kXgbLaneDepth || D < 1 || D > kXgbMaxFeat)
+        return fail(CE_EINVAL, "lane tables: T=%d depth=%d (<= %d) D=%d", T, depth, kXgbLaneDepth, D);
+    if (T == 0) return CE_OK;
+    if (!nodes || !leaves || !table) return fail(CE_EINVAL, "null pointer");
+    hipLaunchKernelGGL(k_xgb_lane_table, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint2*>(nodes), leaves, T, depth, D, reinterpret_cast<uint2*>(table));
+    return check_launch("ce_xgb_lane_table");
+}
+
+extern "C" int ce_xgb_predict_proba_lanes(const void* X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld,
+                                          const uint32_t* table, const int32_t* group_offsets, int32_t G,
+                                          int32_t depth, float base_margin, int32_t C, void* out, ce_dtype out_dt,
+                                          int64_t ld_out, ce_stream_t stream) {
+    if (int rc = xgb_check(X, x_dt, F, D, ld, G, C, out, out_dt, ld_out)) return rc;
+    if (depth < 0 || depth > kXgbLaneDepth)
+        return fail(CE_EINVAL, "XGB lane tables hold depth <= %d, got %d", kXgbLaneDepth, depth);
+    if (!table || !group_offsets) return fail(CE_EINVAL, "null pointer");
+    if (F == 0) return CE_OK;
+    const int S = xgb_splits(G);
+    const XgbArgs a{X, F, D, ld, G, C, S, base_margin, out, ld_out};
+    xgb_dispatch(x_dt, out_dt, [&](auto xd, auto od) {
+        constexpr int XD = decltype(xd)::value, OD = decltype(od)::value;
+        const auto kern = D <= 128 ? k_xgb_lanes<XD, OD, 2>
+                        : D <= 256 ? k_xgb_lanes<XD, OD, 4>
+                        : D <= 320 ? k_xgb_lanes<XD, OD, 5> : k_xgb_lanes<XD, OD, 8>;
+        xgb_launch(kern, F, ce_xgb_lds_bytes(D, G), 64 * G * S, stream, a, reinterpret_cast<const uint2*>(table),
+                   group_offsets, depth);
+    });
+    return check_launch("ce_xgb_predict_proba_lanes");
 }
 
 extern "C" int ce_xgb_expf(const float* x, int64_t n, float* y, ce_stream_t stream) {

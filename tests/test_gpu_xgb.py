@@ -59,6 +59,9 @@ CASES = [
     ("deep_d10", dict(n_rounds=2, num_class=4, max_depth=10, num_feature=64, seed=18, p_stop=0.05), 1_500),
     # depth 5 with an odd feature count: the LDS-staged walk's tree slots sit past an odd-sized tile
     ("odd_features_d5", dict(n_rounds=12, num_class=4, max_depth=5, num_feature=259, seed=19), 2_000),
+    # the lane-table kernel's staging widths (ce_xgb_predict_proba_lanes: 64-feature chunks 2 / 4 / 5 / 8)
+    ("d200_chunks4", dict(n_rounds=10, num_class=4, max_depth=5, num_feature=200, seed=20), 1_000),
+    ("d400_chunks8", dict(n_rounds=10, num_class=3, max_depth=5, num_feature=400, seed=21), 1_000),
 ]
 
 
@@ -158,3 +161,40 @@ def test_xgb_member_in_committee(ce):
     assert np.array_equal(stack.cpu().numpy(), P)
     _, idx = ce.ops.select_mc(stack, 10, "MNC")
     assert np.array_equal(idx.cpu().numpy(), O.oracle_select_mc(P, 10, "MNC")[1])
+
+
+@pytest.mark.parametrize("nan", [0.03, 0.0], ids=["missing", "dense"])
+@pytest.mark.parametrize("name", ["reference_member", "ragged_tail", "three_class", "binary", "stumps",
+                                  "leaves_only", "odd_features_d5", "d200_chunks4", "d400_chunks8"])
+def test_xgb_lane_paths_agree(ce, name, nan):
+    """The three walks of a depth <= 5 forest through the C-ABI directly:
+    ce_xgb_predict_proba (per-tile tables built on the fly) and
+    ce_xgb_predict_proba_lanes over the ce_xgb_lane_table tables (what
+    ops.xgb_predict_proba runs) -- bit-identical to each other and to the
+    restated predictor; the lane ABI refuses a deeper forest."""
+    from ce_amd import _lib
+    from ce_amd.ops import _p, _stream
+
+    kw, F = {c[0]: (c[1], c[2]) for c in CASES}[name]
+    model = synthetic_model(**kw)
+    forest = XgbForest.from_json(model)
+    D = kw["num_feature"]
+    X = dev(frames(F, D, seed=F + 1, nan=nan, model=model))
+    exp = bits(O.oracle_xgb_predict_proba(X.cpu().numpy(), model))
+    lib = _lib.load()
+    nodes, leaves, goff, depth = forest.device_arrays(X.device)
+    G, C = forest.n_groups, forest.n_classes
+    outs = []
+    for lanes in (False, True):
+        out = torch.empty((F, C), dtype=torch.float32, device="cuda")
+        if lanes:
+            rc = lib.ce_xgb_predict_proba_lanes(_p(X), 1, F, D, X.stride(0), _p(forest.lane_table(X.device, D)),
+                                                _p(goff), G, depth, float(forest.base_margin), C, _p(out), 0,
+                                                out.stride(0), _stream(X.device))
+        else:
+            rc = lib.ce_xgb_predict_proba(_p(X), 1, F, D, X.stride(0), _p(nodes), _p(leaves), _p(goff), G, depth,
+                                          float(forest.base_margin), C, _p(out), 0, out.stride(0), _stream(X.device))
+        assert rc == 0
+        outs.append(bits(out.cpu().numpy()))
+    assert np.array_equal(outs[0], exp) and np.array_equal(outs[1], exp), name
+    assert lib.ce_xgb_lane_table(_p(nodes), _p(leaves), 1, 6, D, _p(X), _stream(X.device)) != 0

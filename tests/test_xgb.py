@@ -176,7 +176,7 @@ def test_abi_argument_checks():
     assert lib.ce_xgb_predict_proba(p, 2, 10, 260, 260, p, p, p, 4, 5, f, 4, p, 0, 4, None) == _lib.CE_EINVAL
     assert lib.ce_xgb_predict_proba(p, 1, 0, 260, 260, p, p, p, 1, 5, f, 2, p, 0, 2, None) == _lib.CE_OK
     assert lib.ce_xgb_expf(None, 5, p, None) == _lib.CE_EINVAL
-    assert lib.ce_xgb_lds_bytes(260, 4) == 260 * 64 * 4 + 4 * 64 * 4
+    assert lib.ce_xgb_lds_bytes(260, 4) == 260 * 64 * 4 + 4 * 64 * 4 + 64
 
 
 def test_ops_guard_without_gpu():

@@ -93,12 +93,14 @@ xgb)  # kernel-trace stats + FETCH_SIZE pass of the XGB member (bench_configs --
   ;;
 mpmc)  # PMC passes over the member kernels (tools/members_pmc.py): SQ occupancy/stall/VALU/LDS, TA/TCP gather load
   cd /tmp
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/mpmc_sq" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" > "$OUT/mpmc_sq.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d "$OUT/prof/mpmc_sq" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" ${MPMC_ARGS} > "$OUT/mpmc_sq.log" 2>&1
   step $? "mpmc sq"
-  timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum -d "$OUT/prof/mpmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" > "$OUT/mpmc_ta.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum -d "$OUT/prof/mpmc_ta" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" ${MPMC_ARGS} > "$OUT/mpmc_ta.log" 2>&1
   step $? "mpmc ta"
-  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS -d "$OUT/prof/mpmc_sq2" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" > "$OUT/mpmc_sq2.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS -d "$OUT/prof/mpmc_sq2" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" ${MPMC_ARGS} > "$OUT/mpmc_sq2.log" 2>&1
   step $? "mpmc sq2"
+  timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM -d "$OUT/prof/mpmc_lds" -o run --output-format csv -- python3 "$ROOT/tools/members_pmc.py" ${MPMC_ARGS} > "$OUT/mpmc_lds.log" 2>&1
+  step $? "mpmc lds"
   ;;
 small)  # single-block / small-pool configs: one kernel trace per config + PMC passes of configs[2] (dense)
   cd /tmp

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--frames", type=int, default=4_000_000)
+    ap.add_argument("--only", default="gnb,sgd,xgb", help="comma list of members to launch")
     a = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(1987)
     D, C, F = 260, 4, a.frames
@@ -28,10 +29,14 @@ def main():
     icpt = torch.zeros(C, device="cuda", dtype=torch.float64)
     X = torch.randn((F, D), device="cuda", dtype=torch.float64, generator=g)
     forest = XgbForest.from_json(synthetic_model(n_rounds=100, num_class=4, max_depth=5, num_feature=D))
+    only = set(a.only.split(","))
     for _ in range(a.reps):
-        ops.gnb_predict_proba(X, theta, var, prior)
-        ops.sgd_predict_proba(X, coef, icpt)
-        ops.xgb_predict_proba(X, forest)
+        if "gnb" in only:
+            ops.gnb_predict_proba(X, theta, var, prior)
+        if "sgd" in only:
+            ops.sgd_predict_proba(X, coef, icpt)
+        if "xgb" in only:
+            ops.xgb_predict_proba(X, forest)
     torch.cuda.synchronize()
     print("ok", F, a.reps)
 

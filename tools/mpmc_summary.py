@@ -11,7 +11,7 @@ import sys
 prof, tag = sys.argv[1], sys.argv[2]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 per = {}
-for sub in ("mpmc_sq", "mpmc_ta", "mpmc_sq2"):
+for sub in ("mpmc_sq", "mpmc_ta", "mpmc_sq2", "mpmc_lds"):
     path = os.path.join(prof, sub, "run_counter_collection.csv")
     if not os.path.exists(path):
         continue
