@@ -8,7 +8,8 @@ using namespace ce;
 // ---- fused mix ---------------------------------------------------------------
 extern "C" size_t ce_select_mix_workspace_bytes(int64_t N, int64_t N_h, int32_t q) {
     if (q > CE_MAX_Q) return sort_ws_bytes((N > 0 ? N : 0) + (N_h > 0 ? N_h : 0));
-    return lists_bytes((int64_t)pool_blocks(N) + pool_blocks(N_h), q < 1 ? 1 : q);
+    // (+ kWideSeedBytes: the mix's workspace covers ce_topq_workspace_bytes of its committee part)
+    return lists_bytes((int64_t)pool_blocks(N) + pool_blocks(N_h), q < 1 ? 1 : q) + kWideSeedBytes;
 }
 
 extern "C" int ce_select_mix(const void* p, ce_dtype dt, int64_t N, int32_t M, int32_t C, int64_t sN, int64_t sM,

@@ -102,8 +102,9 @@ static int select_mc_impl(const void* p, ce_dtype dt, int64_t N, int32_t M, int3
         }
         // large pools: the streaming stage 1 with stage 2 folded into its last block
         const int G = pool_blocks(N);
-        const int sr = launch_stream_fold(a, G, q, base_idx, carve(ws, G, q), st, excl,
-                                          FoldOut{val_out, idx_out, nullptr, nullptr, nullptr});
+        const WsLists w = carve(ws, G, q);
+        const int sr = launch_stream_fold(a, G, q, base_idx, w, st, excl,
+                                          FoldOut{val_out, idx_out, nullptr, nullptr, w.c + (int64_t)G * q});
         if (sr == 2) return check_launch("ce_select_mc");
         if (sr == 1) {
             finish_lists(carve(ws, G, q), 1, G, q, val_out, idx_out, st);
@@ -142,7 +143,8 @@ extern "C" int ce_select_mc_cands(const void* p, ce_dtype dt, int64_t N, int32_t
     const int G = pool_blocks(N);
     WsLists w = carve(ws, G, q);
     const int sr =
-        N > 0 ? launch_stream_fold(a, G, q, base_idx, w, st, nullptr, FoldOut{nullptr, nullptr, oc, nullptr, nullptr}) : 0;
+        N > 0 ? launch_stream_fold(a, G, q, base_idx, w, st, nullptr, FoldOut{nullptr, nullptr, oc, nullptr, w.c + (int64_t)G * q})
+              : 0;
     if (sr == 2) return check_launch("ce_select_mc_cands");
     if (sr == 0) {  // no streaming kernel (q > 64, or an empty pool): the block-synchronous stage 1
         Seg sg{nullptr, N, G, base_idx};
@@ -227,7 +229,7 @@ __global__ void k_cand_empty(Cand* __restrict__ c, int q) {
 
 extern "C" size_t ce_select_mc_chunk_workspace_bytes(int64_t N, int32_t q) {
     if (q > CE_MAX_Q) return sort_ws_bytes(N, 2 * (int64_t)q);
-    return lists_bytes((int64_t)pool_blocks(N) + 1, q < 1 ? 1 : q) + 256;  // + the grid vote word
+    return lists_bytes((int64_t)pool_blocks(N) + 1, q < 1 ? 1 : q) + kWideSeedBytes;
 }
 
 // Stage 1 on the chunk (its G block lists), then ONE merge of those G lists
@@ -276,11 +278,9 @@ extern "C" int ce_select_mc_chunk(const void* p, ce_dtype dt, int64_t N, int32_t
     WsLists w = carve(ws, (int64_t)G + 1, q);
     // q <= 64, one launch per chunk: the streaming stage 1 whose last block merges
     // the grid's lists AND the running list back into `running`
-    // the grid vote word (wide seeded chunks): right after the G + 1 lists, inside
-    // the workspace's slack (ce_select_mc_chunk_workspace_bytes)
-    uint32_t* vote = reinterpret_cast<uint32_t*>(w.c + ((int64_t)G + 1) * q);
+    // the wide stream's floor + grid vote scratch: right after the G + 1 lists
     const int sr = launch_stream_fold(a, G, q, base_idx, w, st, nullptr,
-                                      FoldOut{nullptr, nullptr, run, first ? nullptr : run, first ? nullptr : vote});
+                                      FoldOut{nullptr, nullptr, run, first ? nullptr : run, w.c + ((int64_t)G + 1) * q});
     if (sr == 2) return check_launch("ce_select_mc_chunk");
     if (!first && hipMemcpyAsync(w.c + (int64_t)G * q, run, (size_t)q * sizeof(Cand), hipMemcpyDeviceToDevice, st) !=
                       hipSuccess)

@@ -43,6 +43,28 @@ static inline size_t lists_bytes(int64_t nlists, int q) {
     return kWsHeader + (size_t)nlists * (size_t)q * 16u + 256u;
 }
 
+// The wide stream's floor + grid vote scratch (k_wide_seed / k_wide_seed_pick),
+// carved right after a launch's lists: every workspace size that can reach a
+// folded wide launch adds kWideSeedBytes (ce_topq_workspace_bytes,
+// ce_select_mc_chunk_workspace_bytes).
+constexpr size_t kWideSeedBytes = 256 + 256 + (size_t)kWideVoteSamples * (sizeof(Cand) + sizeof(float)) + 256;
+constexpr int64_t kWideSeedMinItems = 16 * 1024;  // >= 1024 samples (wide_nsamples: 1/16 of the items)
+struct WideSeedWs {
+    uint32_t* vote;
+    Cand* seed;
+    Cand* samp;   // [kWideVoteSamples]
+    float* sapx;  // [kWideVoteSamples]
+};
+static inline WideSeedWs wide_seed_carve(void* base) {
+    const uintptr_t p = ((uintptr_t)base + 255) & ~(uintptr_t)255;
+    WideSeedWs w;
+    w.vote = reinterpret_cast<uint32_t*>(p);
+    w.seed = reinterpret_cast<Cand*>(p + 16);
+    w.samp = reinterpret_cast<Cand*>(p + 256);
+    w.sapx = reinterpret_cast<float*>(p + 256 + (size_t)kWideVoteSamples * sizeof(Cand));
+    return w;
+}
+
 struct WsLists {
     Cand* c;        // candidate lists
     uint32_t* ctr;  // arrival counters (header)
@@ -212,6 +234,7 @@ static inline StreamArgs stream_args(const CommArgs& a, int G, int64_t base_idx)
     s.extra = nullptr;
     s.vote = nullptr;
     s.vote_heavy = 0;
+    s.seed = nullptr;
     return s;
 }
 
@@ -246,7 +269,7 @@ struct FoldOut {
     int64_t* oidx;
     Cand* ocand;
     const Cand* extra;  // one more list to merge (a chunked job's running list), or nullptr
-    uint32_t* vote;     // with extra: a device word for the wide stream's grid vote (k_wide_vote), or nullptr
+    void* wide_ws;      // kWideSeedBytes of workspace for the wide stream's floor + grid vote, or nullptr
 };
 CE_HIDDEN int launch_stream_fold(const CommArgs& a, int G, int q, int64_t base_idx, WsLists w, hipStream_t st,
                                  const uint32_t* excl, FoldOut out);

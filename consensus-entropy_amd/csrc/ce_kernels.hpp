@@ -350,62 +350,147 @@ __global__ __launch_bounds__(kBS) void k_stream_wide(WideArgs a, PwPlan pl, Stre
 #ifndef CE_WIDE_PREFILTER
 #define CE_WIDE_PREFILTER 1
 #endif
-// A chunked job's seeded chunks choose their grid on the device (both grids
-// are launched, ce_launch_stream.hip): kWideVoteSamples items spread evenly
-// over the chunk, one wave each, take the prefilter's test against the running
-// list's q-th entry, and *vote counts the ones that would take the exact
-// entropy (every sample when the list is not full yet).  The deep-ring grid
-// (one block per CU, 8-batch ring) reads a chunk whose items nearly all skip
-// at 0.86-0.89 of HBM, but one whose items beat the running floor (e.g. a pool
-// ordered by rising entropy) at 0.51, where the occupancy grid keeps 0.79-0.82
-// (profiles/r06_c5_vote.json): it runs iff at most 1/kWideVoteDen of the
-// samples are exact.  The vote reads ~kWideVoteSamples items (64 MB of a
-// 128 GB C5 chunk).
-constexpr int kWideVoteSamples = 1024;
+// The wide stream's floor and grid, chosen on the device before the stream
+// (ce_launch_stream.hip; every wide launch with heavy items that folds its
+// lists: single selections, the multi-GPU records, every chunk of a job):
+//   k_wide_seed       wide_nsamples(N) items, one per stratum of the pool at a
+//                     hashed offset, one wave each: the EXACT entropy (the
+//                     stream's own arithmetic) and the approximate one;
+//   k_wide_seed_pick  the floor = the better of the samples' q-th best (key,
+//                     any position: every one of those q items is in the pool
+//                     and re-enters the stream's lists, ties included) and a
+//                     chunked job's running q-th entry; then the vote = the
+//                     samples that would still take the exact entropy against it.
+// Both grids are launched; the one the vote does not pick exits at its first
+// instruction.  The deep-ring grid (one block per CU, 8-batch ring) reads a
+// pool whose items nearly all skip at 0.86-0.89 of HBM but one whose items
+// mostly take the exact entropy at 0.51, where the occupancy grid keeps
+// 0.79-0.82 (profiles/r06_c5_vote.json): it runs iff at most 1/kWideVoteDen
+// of the samples are exact.  The sampled floor leaves ~q / kWideVoteSamples of
+// any pool above it whatever the pool's order (a rising-entropy pool included),
+// so single selections and first chunks get the deep grid too.  The samples
+// read 1/16 of a small launch's items and 256 MB of a 128 GB C5 chunk.
+constexpr int kWideVoteSamples = 4096;
 constexpr int kWideVoteDen = 16;
+// samples of an N-item launch: N / 16, at most kWideVoteSamples (the launcher
+// runs the path from 1024 samples on: N >= 16384)
+__host__ __device__ __forceinline__ int64_t wide_nsamples(int64_t N) {
+    return N / 16 < kWideVoteSamples ? N / 16 : kWideVoteSamples;
+}
 __device__ __forceinline__ bool wide_vote_heavy(uint32_t v, int64_t N) {
-    const int64_t ns = N < kWideVoteSamples ? N : kWideVoteSamples;
-    return (int64_t)v * kWideVoteDen <= ns;
+    return (int64_t)v * kWideVoteDen <= wide_nsamples(N);
+}
+// sample s of ns over [0, N): stratum s at a hashed offset (no periodic pool
+// pattern lines up with the samples)
+__host__ __device__ __forceinline__ int64_t wide_sample_pos(int64_t s, int64_t ns, int64_t N) {
+    const int64_t lo = s * N / ns, hi = (s + 1) * N / ns;
+    uint32_t h = (uint32_t)s * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    return hi > lo ? lo + (int64_t)(h % (uint64_t)(hi - lo)) : lo;
 }
 template <int DT, int KCH, int UNR>
-__global__ __launch_bounds__(kBS) void k_wide_vote(WideArgs a, const Cand* __restrict__ extra, int q,
-                                                   uint32_t* __restrict__ vote) {
+__global__ __launch_bounds__(kBS) void k_wide_seed(WideArgs a, PwPlan pl, int64_t base_idx,
+                                                   const uint32_t* __restrict__ excl, Cand* __restrict__ samp,
+                                                   float* __restrict__ sapx) {
+    stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
+    extern __shared__ __attribute__((aligned(16))) double wsm[];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t ns = a.N < kWideVoteSamples ? a.N : kWideVoteSamples;
+    const int64_t ns = wide_nsamples(a.N);
     const int64_t s = (int64_t)blockIdx.x * 4 + w;
-    if (s >= ns) return;  // wave-uniform
-    CE_DASSERT(q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
-    const Cand e = extra[q - 1];
-    bool exact = true;
-    if (e.idx >= 0 && e.key != 0) {
-        constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
-        const int K = a.C / CPC;
-        uint32_t off[KCH];
+    if (s >= ns) return;  // wave-uniform (after the block's only barrier)
+    CE_DASSERT(a.M % UNR == 0);
+    constexpr int CPC = ChunkT<DT>::CPC, EB = 16 / CPC;
+    const int K = a.C / CPC;
+    double* row = wsm + w * wide_lds_doubles(a.C);
+    double* scratch = row + a.C;
+    uint32_t off[KCH];
 #pragma unroll
-        for (int kk = 0; kk < KCH; ++kk) {
-            const int ch = lane + 64 * kk;
-            off[kk] = 16u * (uint32_t)(ch < K ? ch : K - 1);
-        }
-        const char* item = static_cast<const char*>(a.p) + (s * a.N / ns) * a.sN * EB;
-        double acc[KCH * CPC];
-#pragma unroll
-        for (int x = 0; x < KCH * CPC; ++x) acc[x] = 0.0;
-        WideBatch<DT, KCH, UNR> b;
-        for (int m = 0; m < a.M; m += UNR) {  // member order, as the stream adds
-            b.issue(item, m, a.sM * EB, off);
-            b.add(acc);
-        }
-        bool special;
-        const float ap = wave_approx_entropy<DT, KCH>(acc, K, special);
-        exact = special || !(e.key == ~0ull || (double)ap < key_to_val(e.key) * 1.4426950408889634 - 2.0 * kWideApproxErr2);
+    for (int kk = 0; kk < KCH; ++kk) {
+        const int ch = lane + 64 * kk;
+        off[kk] = 16u * (uint32_t)(ch < K ? ch : K - 1);
     }
-    if (lane == 0 && exact) atomicAdd(vote, 1u);
+    const int64_t i = wide_sample_pos(s, ns, a.N);
+    const char* item = static_cast<const char*>(a.p) + i * a.sN * EB;
+    double acc[KCH * CPC];
+#pragma unroll
+    for (int x = 0; x < KCH * CPC; ++x) acc[x] = 0.0;
+    WideBatch<DT, KCH, UNR> b;
+    for (int m = 0; m < a.M; m += UNR) {  // member order, as the stream adds
+        b.issue(item, m, a.sM * EB, off);
+        b.add(acc);
+    }
+    bool special;
+    const float ap = wave_approx_entropy<DT, KCH>(acc, K, special);
+    const double h = wave_entropy_from_sums<DT, KCH>(acc, K, a.dM, a.invM, a.pow2, pl, row, scratch);
+    if (lane == 0) {
+        const bool out = excl != nullptr && excluded(excl, i);
+        samp[s] = Cand{out ? 0ull : order_key(h), i + base_idx};
+        sapx[s] = out ? -__builtin_inff() : (special ? __builtin_inff() : ap);  // -inf: never exact; +inf: always
+    }
+}
+// one block of 16 waves (a template: defined in a header that several
+// translation units include, instantiated in one)
+template <int NS>
+__global__ __launch_bounds__(1024) void k_wide_seed_pick(const Cand* __restrict__ samp, const float* __restrict__ sapx,
+                                                         int ns, int q, const Cand* __restrict__ extra,
+                                                         Cand* __restrict__ seed, uint32_t* __restrict__ vote) {
+    __shared__ WaveListsT<16> sm;
+    __shared__ Cand lst[kStreamMaxQ];
+    __shared__ Cand pick;
+    __shared__ uint32_t cnt;
+    CE_DASSERT(ns <= NS && q >= 1 && q <= kStreamMaxQ && blockDim.x == 1024);
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    // the samples' top q (per-wave register lists over 64-sample rounds, then the
+    // block's merge tree): lst[q - 1] is the q-th best
+    RegTopQ tq;
+    tq.init(q);
+    for (int j0 = w * 64; j0 < ns; j0 += 1024) {  // wave-uniform
+        const int j = j0 + lane;
+        const Cand c = j < ns ? samp[j] : Cand{0ull, -1};
+        tq.offer(c.key, c.idx, j < ns && c.key != 0);
+    }
+    block_merge_write<16>(tq, sm, q, lst, 1);
+    if (t == 0) cnt = 0u;
+    __syncthreads();
+    if (t == 0) {
+        // the q-th best sample as a floor admitting every item of its key (each of
+        // the q samples is in the pool and re-enters the stream's lists, ties
+        // included); a chunked job's running list's q-th entry is a floor too
+        const Cand s = lst[q - 1];
+        Cand f = (s.idx >= 0 && s.key != 0) ? Cand{s.key, INT64_MAX} : Cand{0ull, -1};
+        if (extra != nullptr) {
+            const Cand e = extra[q - 1];
+            if (e.idx >= 0 && e.key != 0 && (f.idx < 0 || better(e.key, e.idx, f.key, f.idx))) f = e;
+        }
+        pick = f;
+    }
+    __syncthreads();
+    const Cand f = pick;
+    // the vote: samples the prefilter would still send to the exact entropy
+    uint32_t mine = 0;
+    for (int j = t; j < ns; j += 1024) {
+        bool exact = true;
+        if (f.idx >= 0 && f.key != 0)
+            exact = !(sapx[j] == -__builtin_inff()) &&
+                    !(f.key == ~0ull || (double)sapx[j] < key_to_val(f.key) * 1.4426950408889634 - 2.0 * kWideApproxErr2);
+        mine += exact ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+    if (lane == 0 && mine) atomicAdd(&cnt, mine);
+    __syncthreads();
+    if (t == 0) {
+        seed[0] = f;
+        vote[0] = cnt;
+    }
 }
 
 template <int DT, int KCH, int UNR, int NB = 2>
 __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, StreamArgs sa, int q,
                                                       Cand* __restrict__ wc) {
-    // a seeded chunk's device-side grid choice (k_wide_vote): the other grid runs
+    // the device-side grid choice (k_wide_seed_pick's vote): the other grid runs
     if (sa.vote && wide_vote_heavy(*sa.vote, sa.N) != (sa.vote_heavy != 0)) return;
     stage_log_table();  // glibc log table -> LDS (ce_glibc_log.hpp)
     CE_DASSERT((int)gridDim.x <= sa.nlists && q >= 1 && q <= kStreamMaxQ && a.M % UNR == 0);
@@ -426,13 +511,13 @@ __global__ __launch_bounds__(kBS) void k_stream_wide2(WideArgs a, PwPlan pl, Str
     RegTopQ tq;
     tq.init(q);
 #if CE_WIDE_PREFILTER
-    // a chunked job's running list (sa.extra: the top q of every chunk so far,
-    // best first) bounds this chunk from below: an item not better than its
-    // q-th entry cannot enter the job's top q -- the exact floor, so the
-    // prefilter skips from the first item on
-    if (sa.extra) {
+    // the floor (k_wide_seed_pick: sampled items, or a chunked job's running
+    // list -- sa.extra, the top q of every chunk so far): an item not better
+    // than it cannot enter the top q, so the prefilter skips from the first
+    // item on
+    if (sa.seed || sa.extra) {
         CE_DASSERT(q >= 1 && q <= kStreamMaxQ);
-        const Cand e = sa.extra[q - 1];
+        const Cand e = sa.seed ? sa.seed[0] : sa.extra[q - 1];
         if (e.idx >= 0 && e.key != 0) tq.init(q, e.key, e.idx);
     }
 #endif

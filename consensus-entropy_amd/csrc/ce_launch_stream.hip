@@ -132,33 +132,35 @@ static int launch_stream_impl(const CommArgs& a, int G, int q, int64_t base_idx,
             // 1 block with a 2-batch ring 0.741, deeper rings at 2 per CU
             // 0.813-0.817, a 12-batch ring spills).  Only 4 waves per CU cannot
             // hide exact entropies, though: with every item exact (the build
-            // without the prefilter) the same grid reads 0.56 against 0.78, so the
-            // first chunk and single selections keep the occupancy grid, and a
-            // seeded chunk runs it only when the grid vote (k_wide_vote) finds at
-            // most 1/16 of its samples beating the running floor: a chunk of
-            // rising entropies (every item exact) read 0.51 on the deep grid,
-            // 0.79-0.82 on the occupancy grid (profiles/r06_c5_vote.json).  A
-            // wave PAIR per item on the deep grid (two waves per SIMD, each half
-            // the classes) was measured and dropped: 0.61 on that pool, 0.77-0.79
-            // where the deep grid reads 0.86-0.89 (the same file).
-            bool seeded = false;  // a chunked job's chunk after the first, heavy items
-            if constexpr (KCH <= 2)   // (wider lanes: 8 batches would spill)
-                seeded = R >= kWideHeavyBytes && fold != nullptr && fold->extra != nullptr &&
-                         fold->vote != nullptr && CE_WIDE_PREFILTER;
-            if (seeded) {
+            // without the prefilter) the same grid reads 0.56 against 0.78, so it
+            // runs only where a floor makes nearly every item skip: the floor is
+            // sampled from the pool itself (and a chunked job's running list),
+            // and the grid vote sends the launch to the occupancy grid when more
+            // than 1/16 of the samples would still be exact -- a chunk order of
+            // rising entropies read 0.51 on the deep grid against 0.79-0.82 on the
+            // occupancy grid (profiles/r06_c5_vote.json).  A wave PAIR per item
+            // on the deep grid (two waves per SIMD, each half the classes) was
+            // measured and dropped: 0.61 on that pool, 0.77-0.79 where the deep
+            // grid reads 0.86-0.89 (the same file).
+            // heavy items in a launch that folds its lists (single selections, the
+            // multi-GPU records, every chunk of a job): the sampled floor + grid
+            // vote (k_wide_seed / k_wide_seed_pick, ce_kernels.hpp), then both grids
+            bool voted = false;
+            if constexpr (KCH <= 2)  // (wider lanes: 8 batches would spill)
+                voted = R >= kWideHeavyBytes && fold != nullptr && fold->wide_ws != nullptr &&
+                        a.N >= kWideSeedMinItems && CE_WIDE_PREFILTER;
+            if (voted) {
                 if constexpr (KCH <= 2) {
-                    // the grid vote (k_wide_vote, ce_kernels.hpp), then both grids:
-                    // the one the vote does not pick exits at its first instruction
-                    const int64_t ns = std::min<int64_t>(a.N, kWideVoteSamples);
-                    if (hipMemsetAsync(fold->vote, 0, sizeof(uint32_t), st) != hipSuccess) {
-                        rc_excl = CE_ELAUNCH;
-                        return;
-                    }
-                    auto vk = unr == UNR ? k_wide_vote<DT, KCH, UNR> : k_wide_vote<DT, KCH, 1>;
-                    hipLaunchKernelGGL(vk, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, st, wa, fold->extra, q,
-                                       fold->vote);
+                    const WideSeedWs sw = wide_seed_carve(fold->wide_ws);
+                    const int ns = (int)wide_nsamples(a.N);
+                    auto sk = unr == UNR ? k_wide_seed<DT, KCH, UNR> : k_wide_seed<DT, KCH, 1>;
+                    hipLaunchKernelGGL(sk, dim3((unsigned)cdiv(ns, 4)), dim3(256), lds, st, wa, pl, sa.base_idx, sa.excl,
+                                       sw.samp, sw.sapx);
+                    hipLaunchKernelGGL(k_wide_seed_pick<kWideVoteSamples>, dim3(1), dim3(1024), 0, st, sw.samp, sw.sapx, ns, q,
+                                       fold->extra, sw.seed, sw.vote);
                     StreamArgs sh = sa, so = sa;
-                    sh.vote = so.vote = fold->vote;
+                    sh.vote = so.vote = sw.vote;
+                    sh.seed = so.seed = sw.seed;
                     sh.vote_heavy = 1;
                     so.vote_heavy = 0;
                     if (unr == UNR) {

@@ -393,11 +393,14 @@ struct StreamArgs {
     int64_t* oidx;
     Cand* ocand;
     const Cand* extra;  // one more list merged by the fold (chunked jobs: the running list), or nullptr
-    // the wide stream's device-side grid choice (a chunked job's seeded chunks,
-    // k_wide_vote): both grids are launched, the one whose role disagrees with
+    // the wide stream's device-side grid choice (heavy items in a folded launch,
+    // k_wide_seed_pick): both grids are launched, the one whose role disagrees with
     // the vote exits at once (nullptr: no vote, the kernel runs)
     const uint32_t* vote;
     int vote_heavy;  // 1: run iff the vote picks the deep-ring grid; 0: iff it does not
+    // the wide stream's prefilter floor (k_wide_seed_pick), one record, or nullptr
+    // (then a chunked job's running list seeds it: extra[q - 1])
+    const Cand* seed;
 };
 
 // Merge the block's WAVES wave lists (registers, best-first) into the

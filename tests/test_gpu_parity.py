@@ -1216,30 +1216,48 @@ def test_chunked_pool_vs_oracle(ce, C, dt, N, chunk):
     assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, 10)[1])
 
 
-@pytest.mark.parametrize("order", ["rising", "falling", "mixed"])
-def test_chunked_grid_vote_orders(ce, order):
-    """The seeded chunks' device-side grid vote (k_wide_vote: the deep-ring
-    grid when at most 1/16 of 1024 sampled items beat the running list's q-th
-    entry, else the occupancy grid; both are launched, one exits): chunks whose
-    entropies rise (every item beats the floor -> occupancy grid), fall (every
-    item skips -> deep grid) and alternate, 32 x 1000 bf16 (64 KB items), with
-    exact ties on the boundaries -- the job equals the oracle either way."""
-    from oracle import ce_oracle as O
-
-    rng = np.random.default_rng({"rising": 61, "falling": 62, "mixed": 63}[order])
-    N, M, C, chunk = 7_200, 32, 1000, 1_200
-    P = synth(rng, N, M, C, np.float32)
-    # K_i classes near 1.0 and the rest near 2^-10: entropy grows with K_i
-    k = 1 + (np.arange(N) * 999) // N
+def _wide_order_pool(rng, order, N, M, C, chunk):
+    """N x M x C f32 rows: item i has K_i classes near 1.0 and the rest near
+    2^-10 (entropy grows with K_i), K_i rising / falling with the position, or
+    rising and falling chunk by chunk; identical rows across each boundary."""
+    k = 1 + (np.arange(N) * (C - 1)) // N
     if order == "falling":
         k = k[::-1]
     elif order == "mixed":
         k = np.concatenate([k[lo:lo + chunk][::(-1) ** (lo // chunk)] for lo in range(0, N, chunk)])
-    base = np.where(np.arange(C)[None, :] < k[:, None], 1.0, 2.0 ** -10)
-    P = (base[:, None, :] * (1.0 + 0.05 * P)).astype(np.float32)
+    base = np.where(np.arange(C)[None, :] < k[:, None], np.float32(1.0), np.float32(2.0 ** -10))
+    P = rng.random((N, M, C), dtype=np.float32)
+    P *= np.float32(0.05)
+    P += np.float32(1.0)
+    P *= base[:, None, :]
     for b in range(chunk, N, chunk):
         P[b - 1:b + 1] = P[b - 2]  # identical rows across each boundary: the earlier position wins
+    return P
+
+
+@pytest.mark.parametrize("order", ["rising", "falling", "mixed", "iid"])
+def test_wide_floor_and_vote_orders(ce, order):
+    """The wide stream's sampled floor + grid vote (k_wide_seed / k_wide_seed_pick:
+    N / 16 (at most 4096) stratified samples' exact entropies give a floor -- better of their
+    q-th and a chunked job's running q-th entry -- the vote sends the launch to
+    the deep-ring grid when at most 1/16 of the samples would still be exact,
+    else to the occupancy grid; both grids are launched, one exits) on pools
+    whose entropies rise, fall or alternate with the position (and i.i.d.),
+    10 x 1000 bf16 (20 KB items, >= 16384 items per launch so every launch takes
+    the path): chunked jobs with ties on the boundaries and single selections
+    equal the oracle, q in {1, 10, 64}."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng({"rising": 61, "falling": 62, "mixed": 63, "iid": 64}[order])
+    N, M, C, chunk = 60_000, 10, 1000, 20_000
+    if order == "iid":
+        P = synth(rng, N, M, C, np.float32)
+        for b in range(chunk, N, chunk):
+            P[b - 1:b + 1] = P[b - 2]
+    else:
+        P = _wide_order_pool(rng, order, N, M, C, chunk)
     host = _bf16_bits(P)
+    del P
     Pd = dev(host.view(np.int16)).view(torch.bfloat16)
     ent_o = O.oracle_committee_entropy(host, "NMC")
     for q in (1, 10, 64):
@@ -1248,7 +1266,48 @@ def test_chunked_grid_vote_orders(ce, order):
         for lo in range(0, N, chunk):
             job.add(Pd[lo:lo + chunk])
         _, idx = job.result()
-        assert np.array_equal(idx_np(idx), idx_o), (order, q)
+        assert np.array_equal(idx_np(idx), idx_o), (order, q, "job")
+        _, idx = ce.ops.select_mc(Pd, q, "NMC")
+        assert np.array_equal(idx_np(idx), idx_o), (order, q, "single")
+
+
+def test_wide_floor_near_ties_and_exclusions(ce):
+    """Pools the sampled floor cannot prune: near-uniform 1000-class rows whose
+    entropies all lie within the approximation's margin of each other (every
+    sample stays exact -> the vote picks the occupancy grid), with NaN rows
+    (all-zero members) and exact duplicates; then the same pool with an
+    exclusion bitmap covering sampled strata (ce_select_mc_excl, the session's
+    path): excluded items never enter the floor nor the selection."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(71)
+    N, M, C = 40_000, 10, 1000
+    P = np.float32(0.5) + np.float32(1e-4) * rng.random((N, M, C), dtype=np.float32)
+    k = rng.permutation(N)
+    P[k[:3]] = 0.0            # NaN entropies: ranked first
+    P[k[3:9]] = P[k[9]]       # exact duplicates
+    host = _bf16_bits(P)
+    del P
+    Pd = dev(host.view(np.int16)).view(torch.bfloat16)
+    ent_o = O.oracle_committee_entropy(host, "NMC")
+    for q in (1, 10, 64):
+        _, idx_o = O.oracle_topq(ent_o, q)
+        _, idx = ce.ops.select_mc(Pd, q, "NMC")
+        assert np.array_equal(idx_np(idx), idx_o), q
+    # exclusions: every other 37-item run plus the NaN rows and the current top 64
+    out = np.zeros(N, dtype=bool)
+    out[(np.arange(N) // 37) % 2 == 0] = True
+    out[k[:3]] = True
+    out[O.oracle_topq(ent_o, 64)[1]] = True
+    excl = ce.ops.excl_bitmap(N, device="cuda")
+    ce.ops.mark_selected(excl, N, torch.from_numpy(np.flatnonzero(out)).cuda())
+    ent_x = ent_o.copy()
+    ent_x[out] = -np.inf
+    for q in (1, 10, 64):
+        _, idx = ce.ops.select_mc(Pd, q, "NMC", excl=excl)
+        got = idx_np(idx)
+        assert not out[got[got >= 0]].any(), q
+        assert np.array_equal(got, O.oracle_topq(ent_x, q)[1]), q
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])

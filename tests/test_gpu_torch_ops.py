@@ -265,27 +265,29 @@ def test_last_kernel_names_the_stage1_kernel(tops):
 
 
 def test_wide_chunks_grid_rule(tops):
-    """The wide stream's grid (csrc/ce_launch_stream.hip): a chunked job's first
-    chunk and single selections run the occupancy grid with a 2-batch ring;
-    the chunks after the first (prefilter seeded by the running list) with
-    >= 16 KiB items launch the grid vote and BOTH grids -- one block per CU
-    with an 8-batch ring, and the occupancy grid; the one the vote does not
-    pick exits at once (ce_last_kernel() names both) -- and the job selects
-    what one launch over the whole pool selects."""
+    """The wide stream's grid (csrc/ce_launch_stream.hip): a launch with heavy
+    items (>= 16 KiB) of >= 16384 items that folds its lists -- every chunk of
+    a job, single selections -- runs the sampled floor + grid vote and launches
+    BOTH grids (one block per CU with an 8-batch ring, and the occupancy grid;
+    the one the vote does not pick exits at once: ce_last_kernel() names both);
+    a smaller launch runs the occupancy grid alone -- and the job selects what
+    one launch over the whole pool selects."""
     import ce_amd
     import ce_amd.ops as ops
 
     lib = ce_amd._lib.load()
     g = torch.Generator(device="cuda").manual_seed(55)
-    P = torch.rand((6000, 32, 1000), device="cuda", generator=g).to(torch.bfloat16)  # 64 KB items
+    P = torch.rand((50_000, 10, 1000), device="cuda", generator=g).to(torch.bfloat16)  # 20 KB items
+    both = "ce::k_stream_wide2<2, 2, 2, 8>|ce::k_stream_wide2<2, 2, 2, 2>"
     job = ops.MCChunkJob(10, "NMC")
-    job.add(P[:2000])
+    job.add(P[:20_000])
+    assert lib.ce_last_kernel().decode() == both
+    job.add(P[20_000:40_000])
+    assert lib.ce_last_kernel().decode() == both
+    job.add(P[40_000:])
     assert lib.ce_last_kernel().decode() == "ce::k_stream_wide2<2, 2, 2, 2>"
-    job.add(P[2000:4000])
-    assert lib.ce_last_kernel().decode() == "ce::k_stream_wide2<2, 2, 2, 8>|ce::k_stream_wide2<2, 2, 2, 2>"
-    job.add(P[4000:])
     v, i = job.result()
     v1, i1 = ops.select_mc(P, 10, "NMC")
-    assert lib.ce_last_kernel().decode() == "ce::k_stream_wide2<2, 2, 2, 2>"
+    assert lib.ce_last_kernel().decode() == both
     torch.cuda.synchronize()
     assert torch.equal(i, i1) and torch.equal(v.view(torch.int64), v1.view(torch.int64))
