@@ -2,11 +2,12 @@
 diagnostic build's stamps (make -C consensus-entropy_amd phase; run with
 CE_AMD_LIB=tools/_diag/ce_amd_phase.so):
   c3  BASELINE configs[2]: 500 users x 4 x 1608 x 4 f32, one launch -> 500 blocks
+  c3cold  the same, 8 distinct pools rotated between launches (each launch reads HBM)
   c1  configs[0]: one 4 x 1608 x 4 f64 pool -> one block; 5 samples, each the
       last of 200 back-to-back launches
 The shader clock over a block = shader-clock ticks / wall-clock (100 MHz) time
 between the block's first and last stamps.
-  python tools/phase_probe.py [c3|c1]"""
+  python tools/phase_probe.py [c3|c3cold|c1]"""
 import ctypes
 import json
 import os
@@ -53,12 +54,12 @@ def reduce(b):
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
     g = torch.Generator(device="cuda").manual_seed(1)
-    if cfg == "c3":
+    if cfg in ("c3", "c3cold"):
         U, Nu = 500, 1608
-        P = torch.rand((4, U * Nu, 4), device="cuda", generator=g)
+        pools = [torch.rand((4, U * Nu, 4), device="cuda", generator=g) for _ in range(8 if cfg == "c3cold" else 1)]
         offs = torch.arange(U + 1, device="cuda", dtype=torch.int64) * Nu
-        for _ in range(20):
-            ops.select_batched(P, offs, 10, "MNC")
+        for it in range(20):  # c3cold: 8 pools rotated (412 MB > the 256 MiB Infinity Cache), stamps of the last
+            ops.select_batched(pools[it % len(pools)], offs, 10, "MNC")
         torch.cuda.synchronize()
         out = reduce(stamps(U))
     else:
