@@ -168,6 +168,56 @@ __device__ __forceinline__ bool stage_tile(const void* X, int64_t F, int D, int6
     return has_nan;
 }
 
+// f64 frames, two features per lane (16-B loads: half the load instructions of
+// stage_tile for the same bytes): lane l takes features 2 l, 2 l + 1 of each
+// 128-feature chunk; the pair is clamped to start <= D - 2 (D >= 2), so every
+// load stays inside the row and is unconditional.  A/B on one box
+// (profiles/r06_xgb.json): 3.279 -> 3.245 ms at 4M frames (dense), 3.418 ->
+// 3.390 ms (missing values).
+#ifndef CE_XGB_PAIRS
+#define CE_XGB_PAIRS 1
+#endif
+template <int KP>  // KP: 128-feature chunks per row, >= ceil(D / 128)
+__device__ __forceinline__ bool stage_tile_pairs(const double* X, int D, int64_t ld, int64_t f0, int nf, float* xs) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, W = blockDim.x >> 6;
+    bool has_nan = false;
+    for (int r0 = w; r0 < kXgbTile; r0 += 2 * W) {  // wave-uniform
+        double2 v[2][KP];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = min(r0 + h * W, kXgbTile - 1);
+            const int64_t row = f0 + min(r, nf - 1);
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+                const int fl = min(2 * lane + 128 * k, D - 2);
+                const double* src = X + row * ld + fl;
+                v[h][k] = make_double2(src[0], src[1]);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = r0 + h * W;
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+                const int f = 2 * lane + 128 * k, fl = min(f, D - 2);
+                if (r < kXgbTile) {
+                    if (f < D) {  // f > fl only for f = D - 1 (odd D): the pair's second value
+                        const float x = (float)(f == fl ? v[h][k].x : v[h][k].y);
+                        xs[f * kXgbCol + (r ^ (f & 63))] = x;
+                        has_nan |= __builtin_isnan(x);
+                    }
+                    if (f + 1 < D && f == fl) {
+                        const float x = (float)v[h][k].y;
+                        xs[(f + 1) * kXgbCol + (r ^ ((f + 1) & 63))] = x;
+                        has_nan |= __builtin_isnan(x);
+                    }
+                }
+            }
+        }
+    }
+    return has_nan;
+}
+
 // The objective's transform of the G margins mg[g * 64 + lane] of frame f0 +
 // lane, written to out (wave 0, one frame per lane).
 template <int ODT>
@@ -562,7 +612,15 @@ __device__ __forceinline__ void xgb_tile(const XgbArgs& a, const L& fl) {
     const int g = w / a.S, s = w - g * a.S;
     const int64_t f0 = (int64_t)blockIdx.x * kXgbTile;
     const int nf = (int)min<int64_t>(kXgbTile, a.F - f0);
-    const bool has_nan = stage_tile<XDT, KF>(a.X, a.F, a.D, a.ld, f0, nf, xs);
+    bool has_nan;
+    if constexpr (XDT == CE_F64 && CE_XGB_PAIRS && KF < kXgbMaxFeat / 64) {  // (the lane-table kernel's widths)
+        if (a.D >= 2)
+            has_nan = stage_tile_pairs<(KF + 1) / 2>(static_cast<const double*>(a.X), a.D, a.ld, f0, nf, xs);
+        else
+            has_nan = stage_tile<XDT, KF>(a.X, a.F, a.D, a.ld, f0, nf, xs);
+    } else {
+        has_nan = stage_tile<XDT, KF>(a.X, a.F, a.D, a.ld, f0, nf, xs);
+    }
     // the block's "any NaN" vote through the dynamic LDS (__syncthreads_or keeps
     // a static LDS word, which puts the tile 256 B off address 0: one more VALU
     // per node read)

@@ -200,11 +200,11 @@ framesab)  # the frames probe (tools/gather_probe.py) per library build (LIBS="b
     done
   done
   ;;
-memab)  # member-inference configs (bench_configs.py --only 6: GNB, SGD) per library build (LIBS="base x"), alternating, 2 rounds
+memab)  # member-inference configs (bench_configs.py --only ${ONLY:-6}: 6 GNB, SGD; 7 XGB) per library build (LIBS="base x"), alternating, 2 rounds
   for rep in 1 2; do
     for lib in ${LIBS:-base}; do
       if [ "$lib" = base ]; then L=$ROOT/consensus-entropy_amd/ce_amd/libce_amd.so; else L=$ROOT/tools/_diag/libce_amd_$lib.so; fi
-      CE_AMD_LIB=$L timeout -k 10 200 python3 tools/bench_configs.py --only 6 > "$OUT/memab_${lib}_$rep.log" 2>&1
+      CE_AMD_LIB=$L timeout -k 10 200 python3 tools/bench_configs.py --only ${ONLY:-6} > "$OUT/memab_${lib}_$rep.log" 2>&1
       step $? "memab $lib $rep"
     done
   done
