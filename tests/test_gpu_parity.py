@@ -1271,6 +1271,25 @@ def test_wide_floor_and_vote_orders(ce, order):
         assert np.array_equal(idx_np(idx), idx_o), (order, q, "single")
 
 
+def test_wide_floor_records_shards(ce):
+    """The multi-GPU records path on a wide pool (ce_select_mc_cands: every
+    shard a folded wide launch with its own sampled floor + grid vote): three
+    shards of a rising-entropy pool at their global offsets, their q records
+    merged (ce_merge_cands), equal the oracle over the whole pool, q in {1, 10,
+    64}; the shard holding the top items and the ones holding none both count."""
+    from oracle import ce_oracle as O
+
+    rng = np.random.default_rng(81)
+    N, M, C, shard = 54_000, 10, 1000, 18_000
+    host = _bf16_bits(_wide_order_pool(rng, "rising", N, M, C, shard))
+    Pd = dev(host.view(np.int16)).view(torch.bfloat16)
+    ent_o = O.oracle_committee_entropy(host, "NMC")
+    for q in (1, 10, 64):
+        recs = [ce.ops.MCPlan(Pd[lo:lo + shard], q, "NMC", base_idx=lo).step_cands() for lo in range(0, N, shard)]
+        _, idx = ce.ops.merge_cands(torch.cat(recs).contiguous(), q)
+        assert np.array_equal(idx_np(idx), O.oracle_topq(ent_o, q)[1]), q
+
+
 def test_wide_floor_near_ties_and_exclusions(ce):
     """Pools the sampled floor cannot prune: near-uniform 1000-class rows whose
     entropies all lie within the approximation's margin of each other (every
