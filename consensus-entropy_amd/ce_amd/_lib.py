@@ -40,7 +40,7 @@ SIGNATURES = {
     "ce_xgb_predict_proba": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _vp, _vp, _i32, _i32, ctypes.c_float, _i32,
                                     _vp, _int, _i64, _vp]),
     "ce_xgb_lane_table": (_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp]),
-    "ce_xgb_predict_proba_lanes": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _vp, _i32, _i32, ctypes.c_float, _i32,
+    "ce_xgb_predict_proba_lanes": (_int, [_vp, _int, _i64, _i32, _i64, _vp, _i32, _vp, _i32, _i32, ctypes.c_float, _i32,
                                           _vp, _int, _i64, _vp]),
     "ce_xgb_lds_bytes": (_sz, [_i32, _i32]),
     "ce_xgb_expf": (_int, [_vp, _i64, _vp, _vp]),

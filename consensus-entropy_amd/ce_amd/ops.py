@@ -524,8 +524,9 @@ def xgb_predict_proba(X, forest, out=None, out_dtype=torch.float32):
     nodes, leaves, goff, depth = forest.device_arrays(X.device)
     if depth <= LANE_TABLE_DEPTH:  # the reference's max_depth=5: prebuilt per-tree lane tables
         table = forest.lane_table(X.device, D)
-        call("ce_xgb_predict_proba_lanes", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(table), _p(goff), G, depth,
-             float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0), _stream(X.device))
+        call("ce_xgb_predict_proba_lanes", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(table), table.shape[1],
+             _p(goff), G, depth, float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0),
+             _stream(X.device))
     else:
         call("ce_xgb_predict_proba", _p(X), _DT[X.dtype], F, D, X.stride(0), _p(nodes), _p(leaves), _p(goff), G,
              depth, float(forest.base_margin), C, _p(out), _DT[out.dtype], out.stride(0), _stream(X.device))

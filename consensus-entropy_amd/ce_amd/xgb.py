@@ -185,8 +185,9 @@ class XgbForest:
 
     def lane_table(self, device, D):
         """The prebuilt per-tree lane tables of ce_xgb_predict_proba_lanes (depth
-        <= 5): int32 [T, 64, 2] on ``device`` for X with D columns, built once on
-        the device by ce_xgb_lane_table and cached per (device, D)."""
+        <= 5): int32 [2, T, 64, 2] on ``device`` for X with D columns (with and
+        without the default-left bits), built once on the device by
+        ce_xgb_lane_table and cached per (device, D)."""
         import torch
 
         from . import _lib
@@ -196,7 +197,7 @@ class XgbForest:
         if key not in self._dev:
             nodes, leaves, _, d = self.device_arrays(device)
             T = len(self.trees)
-            table = torch.empty((T, 64, 2), dtype=torch.int32, device=key[0])
+            table = torch.empty((2, T, 64, 2), dtype=torch.int32, device=key[0])
             _lib.load()
             call("ce_xgb_lane_table", _p(nodes), _p(leaves), T, d, int(D), _p(table), _stream(key[0]))
             self._dev[key] = table

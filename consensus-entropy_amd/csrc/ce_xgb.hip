@@ -446,17 +446,19 @@ struct LaneForest {
 // coalesced dwordx2 load with a scalar base is a tree's whole table (no
 // per-lane branches or feature arithmetic), the root comes from a scalar load,
 // and a level is child = 2 j + right.  VALU per tree was the limiter of the
-// on-the-fly tables (PMC r06: VALU 72 % busy, 80 VALU per tree and wave).
+// on-the-fly tables (PMC r06: VALU 72 % busy, 80 VALU per tree and wave).  Two
+// halves [2][T][64]: the second without the default_left bits, read by tiles
+// without a missing value (no mask per node read).
 struct LaneTableForest {
-    const uint2* table;   // [T][64]
+    const uint2* table;     // [T][64], fx with default_left in bit 31 (tiles holding a missing value)
+    const uint2* table_nd;  // [T][64], fx without it (the other tiles: no mask per node read)
     const int32_t* goff;
     int depth, NI;
     int goff_end;
 
-    // fx carries default_left in bit 31 either way (masked in the address: one v_bitop3)
     template <bool MISS>
     static __device__ __forceinline__ bool right(uint32_t fx, uint32_t th, const float* xs, uint32_t lane4) {
-        const float x = xs_at(xs, fx & 0x7fffffffu, lane4);
+        const float x = xs_at(xs, MISS ? (fx & 0x7fffffffu) : fx, lane4);
         // missing -> the default child, else fvalue < split_cond ? left : right; a
         // NaN fails the compare (right), so flip exactly the NaN lanes whose default
         // is left: three compares and two mask ops
@@ -475,9 +477,10 @@ struct LaneTableForest {
     __device__ __forceinline__ void walk8(const float* xs, int D, int t0, int t1, int lane, int (&li)[8],
                                           float (&v)[8]) const {
         (void)D;
+        const uint2* tb = MISS ? table : table_nd;
         uint2 e[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = table[(int64_t)(t0 + j < t1 ? t0 + j : t1 - 1) * 64 + lane];
+        for (int j = 0; j < 8; ++j) e[j] = tb[(int64_t)(t0 + j < t1 ? t0 + j : t1 - 1) * 64 + lane];
         const uint32_t lane4 = 4u * (uint32_t)lane;
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
@@ -490,7 +493,7 @@ struct LaneTableForest {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int t = t0 + 4 * g + j < t1 ? t0 + 4 * g + j : t1 - 1;
-                const uint4* p = reinterpret_cast<const uint4*>(table + (int64_t)t * 64);
+                const uint4* p = reinterpret_cast<const uint4*>(tb + (int64_t)t * 64);
                 q0[j] = p[0];
                 q1[j] = p[1];
             }
@@ -660,14 +663,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 // is unconditional, so a smaller KF drops dead loads: D = 260 takes 5 of 8)
 template <int XDT, int ODT, int KF>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_xgb_lanes(
-    XgbArgs a, const uint2* __restrict__ table, const int32_t* __restrict__ goff, int depth) {
+    XgbArgs a, const uint2* __restrict__ table, const uint2* __restrict__ table_nd, const int32_t* __restrict__ goff,
+    int depth) {
 #ifdef CE_DEBUG
     const int T = goff[a.G];
 #else
     const int T = 0;
 #endif
     CE_DASSERT(depth <= kXgbLaneDepth);
-    xgb_tile<XDT, ODT, LaneTableForest, KF>(a, LaneTableForest{table, goff, depth, (1 << depth) - 1, T});
+    xgb_tile<XDT, ODT, LaneTableForest, KF>(a, LaneTableForest{table, table_nd, goff, depth, (1 << depth) - 1, T});
 }
 
 // ce_xgb_lane_table: one wave per tree, lane j writes heap entry j
@@ -677,14 +681,17 @@ __global__ __launch_bounds__(256) void k_xgb_lane_table(const uint2* __restrict_
     const int j = threadIdx.x & 63, NI = (1 << depth) - 1;
     if (t >= T) return;
     uint2 e = make_uint2(0u, 0u);
+    uint32_t dl = 0u;
     if (j >= 1 && j <= NI) {
         const uint2 nd = nodes[t * NI + (j - 1)];
         const uint32_t ft = min(nd.x & 0x7fffffffu, (uint32_t)(D - 1));
-        e = make_uint2(xs_fbase(ft) | (nd.x & 0x80000000u), nd.y);
+        e = make_uint2(xs_fbase(ft), nd.y);
+        dl = nd.x & 0x80000000u;
     } else if (j >= NI + 1 && j <= 2 * NI + 1) {
         e = make_uint2(0u, __float_as_uint(leaves[t * (NI + 1) + (j - NI - 1)]));
     }
-    table[t * 64 + j] = e;
+    table[t * 64 + j] = make_uint2(e.x | dl, e.y);  // half 0: with default_left
+    table[((int64_t)T + t) * 64 + j] = e;           // half 1: without
 }
 
 __global__ void k_expf(const float* __restrict__ x, int64_t n, float* __restrict__ y) {
@@ -763,23 +770,24 @@ extern "C" int ce_xgb_lane_table(const uint32_t* nodes, const float* leaves, int
 }
 
 extern "C" int ce_xgb_predict_proba_lanes(const void* X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld,
-                                          const uint32_t* table, const int32_t* group_offsets, int32_t G,
+                                          const uint32_t* table, int32_t T, const int32_t* group_offsets, int32_t G,
                                           int32_t depth, float base_margin, int32_t C, void* out, ce_dtype out_dt,
                                           int64_t ld_out, ce_stream_t stream) {
     if (int rc = xgb_check(X, x_dt, F, D, ld, G, C, out, out_dt, ld_out)) return rc;
     if (depth < 0 || depth > kXgbLaneDepth)
         return fail(CE_EINVAL, "XGB lane tables hold depth <= %d, got %d", kXgbLaneDepth, depth);
-    if (!table || !group_offsets) return fail(CE_EINVAL, "null pointer");
+    if (!table || !group_offsets || T < 1) return fail(CE_EINVAL, "null pointer or no trees (T=%d)", T);
     if (F == 0) return CE_OK;
     const int S = xgb_splits(G);
+    const uint2* tb = reinterpret_cast<const uint2*>(table);
     const XgbArgs a{X, F, D, ld, G, C, S, base_margin, out, ld_out};
     xgb_dispatch(x_dt, out_dt, [&](auto xd, auto od) {
         constexpr int XD = decltype(xd)::value, OD = decltype(od)::value;
         const auto kern = D <= 128 ? k_xgb_lanes<XD, OD, 2>
                         : D <= 256 ? k_xgb_lanes<XD, OD, 4>
                         : D <= 320 ? k_xgb_lanes<XD, OD, 5> : k_xgb_lanes<XD, OD, 8>;
-        xgb_launch(kern, F, ce_xgb_lds_bytes(D, G), 64 * G * S, stream, a, reinterpret_cast<const uint2*>(table),
-                   group_offsets, depth);
+        xgb_launch(kern, F, ce_xgb_lds_bytes(D, G), 64 * G * S, stream, a, tb, tb + (int64_t)T * 64, group_offsets,
+                   depth);
     });
     return check_launch("ce_xgb_predict_proba_lanes");
 }

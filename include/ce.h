@@ -191,9 +191,9 @@ int ce_sgd_predict_proba(const double *X, int64_t F, int32_t D, int64_t ld, cons
  *   ce_xgb_expf       the restated glibc expf over x [n] -> y [n] (verification)
  * Forests of depth <= 5 (the reference's XGBClassifier(max_depth=5)) run
  * faster from prebuilt lane tables: ce_xgb_lane_table turns (nodes, leaves)
- * of T trees into table [T][64][2] u32 (T * 512 bytes, device memory) for X
- * with D columns, once per forest; ce_xgb_predict_proba_lanes then takes the
- * table in place of nodes / leaves and must be given the same D.  Same
+ * of T trees into table [2][T][64][2] u32 (T * 1024 bytes, device memory) for
+ * X with D columns, once per forest; ce_xgb_predict_proba_lanes then takes the
+ * table and T in place of nodes / leaves and must be given the same D.  Same
  * results as ce_xgb_predict_proba, bit for bit.
  */
 int ce_xgb_predict_proba(const void *X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld,
@@ -203,7 +203,7 @@ int ce_xgb_predict_proba(const void *X, ce_dtype x_dt, int64_t F, int32_t D, int
 int ce_xgb_lane_table(const uint32_t *nodes, const float *leaves, int32_t T, int32_t depth, int32_t D,
                       uint32_t *table, ce_stream_t stream);
 int ce_xgb_predict_proba_lanes(const void *X, ce_dtype x_dt, int64_t F, int32_t D, int64_t ld,
-                               const uint32_t *table, const int32_t *group_offsets, int32_t G,
+                               const uint32_t *table, int32_t T, const int32_t *group_offsets, int32_t G,
                                int32_t depth, float base_margin, int32_t C, void *out, ce_dtype out_dt,
                                int64_t ld_out, ce_stream_t stream);
 size_t ce_xgb_lds_bytes(int32_t D, int32_t G);

@@ -188,9 +188,10 @@ def test_xgb_lane_paths_agree(ce, name, nan):
     for lanes in (False, True):
         out = torch.empty((F, C), dtype=torch.float32, device="cuda")
         if lanes:
-            rc = lib.ce_xgb_predict_proba_lanes(_p(X), 1, F, D, X.stride(0), _p(forest.lane_table(X.device, D)),
-                                                _p(goff), G, depth, float(forest.base_margin), C, _p(out), 0,
-                                                out.stride(0), _stream(X.device))
+            table = forest.lane_table(X.device, D)
+            rc = lib.ce_xgb_predict_proba_lanes(_p(X), 1, F, D, X.stride(0), _p(table), table.shape[1], _p(goff), G,
+                                                depth, float(forest.base_margin), C, _p(out), 0, out.stride(0),
+                                                _stream(X.device))
         else:
             rc = lib.ce_xgb_predict_proba(_p(X), 1, F, D, X.stride(0), _p(nodes), _p(leaves), _p(goff), G, depth,
                                           float(forest.base_margin), C, _p(out), 0, out.stride(0), _stream(X.device))
