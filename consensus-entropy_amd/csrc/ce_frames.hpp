@@ -356,28 +356,37 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                                                              16, 0, 2);
                         }
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        const int64_t r0 = f0 > c0 ? f0 : c0, r1 = f1 < c1 ? f1 : c1;
                         // this lane's song's rows in the tile, in order: 8 LDS reads in flight,
                         // then the 8 adds (a read per row would wait out an LDS round trip each);
-                        // rows past r1 re-read the tile's first row and are skipped
-                        for (int64_t rb = r0; rb < r1; rb += 8) {
-                            double v[8];
+                        // rows past lr1 re-read the tile's first row and are skipped.  Row
+                        // indices relative to the tile (32-bit) and the element size a
+                        // compile-time constant (one loop per dtype, chosen once per tile:
+                        // a per-row dtype select put a branch and an LDS wait on every row)
+                        const int lr0 = (int)((f0 > c0 ? f0 : c0) - c0);
+                        const int lr1 = (int)((f1 < c1 ? f1 : c1) - c0);  // < lr0: no row of this song here
+                        auto add_rows = [&](auto eb) {
+                            constexpr int EBc = decltype(eb)::value, RBc = C * EBc;
+                            for (int rb = lr0; rb < lr1; rb += 8) {
+                                double v[8];
 #pragma unroll
-                            for (int u8 = 0; u8 < 8; ++u8) {
-                                const int64_t r = rb + u8 < r1 ? rb + u8 : c0;
-                                const int b = (int)(r - c0) * RB + c * EB;
-                                const int u = b >> 4;
-                                const char* e = tile + ((u ^ ((u >> 4) & 15)) << 4) + (b & 15);
-                                v[u8] = EB == 8 ? *reinterpret_cast<const double*>(e)
-                                                : (double)*reinterpret_cast<const float*>(e);
-                            }
-#pragma unroll
-                            for (int u8 = 0; u8 < 8; ++u8)
-                                if (rb + u8 < r1 && v[u8] == v[u8]) {  // not NaN
-                                    s += v[u8];
-                                    ++cnt;
+                                for (int u8 = 0; u8 < 8; ++u8) {
+                                    const int r = rb + u8 < lr1 ? rb + u8 : 0;
+                                    const int b = r * RBc + c * EBc;
+                                    const int u = b >> 4;
+                                    const char* e = tile + ((u ^ ((u >> 4) & 15)) << 4) + (b & 15);
+                                    v[u8] = EBc == 8 ? *reinterpret_cast<const double*>(e)
+                                                     : (double)*reinterpret_cast<const float*>(e);
                                 }
-                        }
+#pragma unroll
+                                for (int u8 = 0; u8 < 8; ++u8)
+                                    if (rb + u8 < lr1 && v[u8] == v[u8]) {  // not NaN
+                                        s += v[u8];
+                                        ++cnt;
+                                    }
+                            }
+                        };
+                        if (EB == 8) add_rows(std::integral_constant<int, 8>());
+                        else add_rows(std::integral_constant<int, 4>());
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the next DMA
                         __builtin_amdgcn_sched_barrier(0);
                     }
