@@ -8,8 +8,9 @@ permutation?  Times, on the configuration of tools/bench_configs.py --only 8
   fused          ops.select_frames(..., perm=perm) (k_frames_lanes, one pass)
   fused_grouped  the same frames already grouped (no perm, LDS-DMA tiles)
 and prints the useful bytes per second of each (rows read once + perm once).
-  python tools/gather_probe.py [--songs N] [--pmc]   (--pmc: only 5 fused shuffled calls, for a
-                                          rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass)"""
+  python tools/gather_probe.py [--songs N] [--mixed] [--pmc]
+  (--mixed: the third frame member float32, as an XGB member's predict_proba;
+   --pmc: only 5 fused shuffled calls, for a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass)"""
 import json
 import os
 import statistics
@@ -40,18 +41,20 @@ def main():
     songs = int(sys.argv[sys.argv.index("--songs") + 1]) if "--songs" in sys.argv else 1_000_000
     fps, C = 40, 4
     F = songs * fps
-    fr = [torch.rand((F, C), dtype=torch.float64, device="cuda", generator=g) for _ in range(3)]
+    mixed = "--mixed" in sys.argv
+    dts = [torch.float64, torch.float64, torch.float32 if mixed else torch.float64]
+    fr = [torch.rand((F, C), dtype=dt, device="cuda", generator=g) for dt in dts]
     cnn = torch.rand((songs, C), dtype=torch.float64, device="cuda", generator=g)
     offs = torch.arange(0, F + 1, fps, device="cuda", dtype=torch.int64)
     perm = torch.randperm(F, device="cuda", generator=g)
-    rows = 3 * F * C * 8
+    rows = sum(f.numel() * f.element_size() for f in fr)
     if "--pmc" in sys.argv:
         for _ in range(5):
             ops.select_frames(fr + [cnn], offs, 10, perm=perm)
         torch.cuda.synchronize()
         print(json.dumps({"pmc_run": "fused shuffled x5", "useful_bytes_per_call": rows + F * 8 + songs * C * 8}))
         return
-    out = {"config": f"{songs} songs x {fps} frames, 3 frame-level f64 members (C={C}, 32-B rows) + 1 song-level"}
+    out = {"config": f"{songs} songs x {fps} frames, 3 frame-level members ({'f64, f64, f32' if mixed else 'f64'}; C={C}) + 1 song-level"}
     reps = 200 if songs < 100_000 else 20
     t = timed(lambda: [torch.index_select(f, 0, perm) for f in fr], reps)
     out["torch_gather"] = {"s": t, "useful_GB_per_s": (rows + 3 * F * 8) / t / 1e9,
