@@ -83,7 +83,9 @@ extern "C" int ce_select_frames(const ce_member* members, int32_t M, int32_t C, 
     fa.oidx = idx_out;
     fa.ocand = nullptr;
     auto go = [&](auto kern, int step) {  // step: songs per wave step (64 / lanes per song)
-        const int grid = resident_grid(kern, 0, G);
+        // no more blocks than waves with a step of songs: an idle block still
+        // writes an empty list that the grid's last block merges
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(resident_grid(kern, 0, G), cdiv(N, (int64_t)4 * step)));
         fa.per_wave = (cdiv(N, (int64_t)grid * 4) + step - 1) / step * step;
         hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, fa, q, w.c);
     };

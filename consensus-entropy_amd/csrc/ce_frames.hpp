@@ -187,6 +187,61 @@ __global__ __launch_bounds__(256) void k_frames_entropy(FrameArgs a, double* __r
     }
 }
 
+// The sum and non-NaN count of column c of this lane's song (rows [f0, f1)
+// of a grouped dense member: rows of C elements of EB bytes, 16-B aligned,
+// base mb), with the wave's step of songs covering rows [R0, R1): the rows are
+// staged TB bytes at a time by LDS-DMA (1 KiB per global_load_lds, fully
+// coalesced) into the wave's tile, 16-B units XOR-swizzled within 256 B, and
+// every lane adds its song's rows of the tile in row order, NaN skipped
+// (pandas group_mean).  Lanes whose song is not in [R0, R1) read no row.
+template <int C, int EB, int TB>
+__device__ __forceinline__ void tile_song_sum(const char* mb, int64_t R0, int64_t R1, int64_t f0, int64_t f1,
+                                              int lane, int c, char* tile, double& s, int& cnt) {
+    constexpr int RB = C * EB, TR = TB / RB;  // bytes per row, rows per tile
+    static_assert(RB % 16 == 0, "16-B units");
+    for (int64_t c0 = R0; c0 < R1; c0 += TR) {
+        const int64_t c1 = c0 + TR < R1 ? c0 + TR : R1;
+        const int units = (int)(c1 - c0) * RB / 16;
+        const char* src = mb + c0 * RB;
+        for (int j = 0; j * 64 < units; ++j) {  // wave-uniform
+            const int pd = j * 64 + lane;  // LDS unit written by this lane
+            int ps = pd ^ ((pd >> 4) & 15);  // its source unit (the swizzle is an involution)
+            ps = ps < units ? ps : units - 1;
+            CE_DASSERT(j * 1024 + 1024 <= TB);
+            __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)ps * 16),
+                                             (void __attribute__((address_space(3)))*)(tile + j * 1024), 16, 0, 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // this lane's song's rows in the tile, in order: 8 LDS reads in flight,
+        // then the 8 adds (a read per row would wait out an LDS round trip each);
+        // rows past lr1 re-read the tile's first row and are skipped.  Row
+        // indices relative to the tile (32-bit) and the element size a
+        // compile-time constant (a per-row dtype select put a branch and an LDS
+        // wait on every row: grouped frames 0.879 -> 0.712 ms, r06_frames_ab.json)
+        const int lr0 = (int)((f0 > c0 ? f0 : c0) - c0);
+        const int lr1 = (int)((f1 < c1 ? f1 : c1) - c0);  // < lr0: no row of this song here
+        for (int rb = lr0; rb < lr1; rb += 8) {
+            double v[8];
+#pragma unroll
+            for (int u8 = 0; u8 < 8; ++u8) {
+                const int r = rb + u8 < lr1 ? rb + u8 : 0;
+                const int b = r * RB + c * EB;
+                const int u = b >> 4;
+                const char* e = tile + ((u ^ ((u >> 4) & 15)) << 4) + (b & 15);
+                v[u8] = EB == 8 ? *reinterpret_cast<const double*>(e) : (double)*reinterpret_cast<const float*>(e);
+            }
+#pragma unroll
+            for (int u8 = 0; u8 < 8; ++u8)
+                if (rb + u8 < lr1 && v[u8] == v[u8]) {  // not NaN
+                    s += v[u8];
+                    ++cnt;
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the next DMA
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // The same selection with C lanes per song (lane = (song, class), 64 / C songs
 // per wave step): each lane keeps ONE class's sequential group sum, so the
 // frame rows of the wave's songs are read as whole rows.  Grouped frames (no
@@ -340,55 +395,11 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
                 // (offsets not monotone) reads its rows directly instead
                 const bool inside = !live || (f0 >= R0 && f1 <= R1);
                 if (DMA && !a.perm && fm.ld == C && RB % 16 == 0 && fm.vec && __all(inside)) {  // wave-uniform: LDS-DMA tiles
-                    const int TR = TB / RB;  // rows per tile
                     const char* mb = static_cast<const char*>(fm.p);
-                    for (int64_t c0 = R0; c0 < R1; c0 += TR) {
-                        const int64_t c1 = c0 + TR < R1 ? c0 + TR : R1;
-                        const int units = (int)(c1 - c0) * RB / 16;
-                        const char* src = mb + c0 * RB;
-                        for (int j = 0; j * 64 < units; ++j) {  // wave-uniform
-                            const int pd = j * 64 + lane;  // LDS unit written by this lane
-                            int ps = pd ^ ((pd >> 4) & 15);  // its source unit (the swizzle is an involution)
-                            ps = ps < units ? ps : units - 1;
-                            CE_DASSERT(j * 1024 + 1024 <= TB);
-                            __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)ps * 16),
-                                                             (void __attribute__((address_space(3)))*)(tile + j * 1024),
-                                                             16, 0, 2);
-                        }
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        // this lane's song's rows in the tile, in order: 8 LDS reads in flight,
-                        // then the 8 adds (a read per row would wait out an LDS round trip each);
-                        // rows past lr1 re-read the tile's first row and are skipped.  Row
-                        // indices relative to the tile (32-bit) and the element size a
-                        // compile-time constant (one loop per dtype, chosen once per tile:
-                        // a per-row dtype select put a branch and an LDS wait on every row)
-                        const int lr0 = (int)((f0 > c0 ? f0 : c0) - c0);
-                        const int lr1 = (int)((f1 < c1 ? f1 : c1) - c0);  // < lr0: no row of this song here
-                        auto add_rows = [&](auto eb) {
-                            constexpr int EBc = decltype(eb)::value, RBc = C * EBc;
-                            for (int rb = lr0; rb < lr1; rb += 8) {
-                                double v[8];
-#pragma unroll
-                                for (int u8 = 0; u8 < 8; ++u8) {
-                                    const int r = rb + u8 < lr1 ? rb + u8 : 0;
-                                    const int b = r * RBc + c * EBc;
-                                    const int u = b >> 4;
-                                    const char* e = tile + ((u ^ ((u >> 4) & 15)) << 4) + (b & 15);
-                                    v[u8] = EBc == 8 ? *reinterpret_cast<const double*>(e)
-                                                     : (double)*reinterpret_cast<const float*>(e);
-                                }
-#pragma unroll
-                                for (int u8 = 0; u8 < 8; ++u8)
-                                    if (rb + u8 < lr1 && v[u8] == v[u8]) {  // not NaN
-                                        s += v[u8];
-                                        ++cnt;
-                                    }
-                            }
-                        };
-                        if (EB == 8) add_rows(std::integral_constant<int, 8>());
-                        else add_rows(std::integral_constant<int, 4>());
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the next DMA
-                        __builtin_amdgcn_sched_barrier(0);
+                    if (EB == 8) {
+                        if constexpr (DMA && (C * 8) % 16 == 0) tile_song_sum<C, 8, TB>(mb, R0, R1, f0, f1, lane, c, tile, s, cnt);
+                    } else {
+                        if constexpr (DMA && (C * 4) % 16 == 0) tile_song_sum<C, 4, TB>(mb, R0, R1, f0, f1, lane, c, tile, s, cnt);
                     }
                 } else {  // direct loads: batches of 8 rows in flight, added in row order
                     constexpr int B = 8;
@@ -429,6 +440,52 @@ __global__ __launch_bounds__(256) void k_frames_lanes(FrameArgs a, int q, Cand* 
     }
     block_merge_write<4>(tq, sm, q, wc + (int64_t)blockIdx.x * q, a.nlists, nullptr, nullptr, 4, a.ctr != nullptr);
     if (a.ctr) fold_merge<4>(a.ctr, a.oval, a.oidx, a.ocand, q, wc, sm);
+}
+
+// frame -> song segment mean of one grouped dense member (ce_segment_mean,
+// amg_test.py:437; the same values as k_segment_mean): C lanes per song, the
+// step's songs' rows staged by LDS-DMA tiles (tile_song_sum), a wave holding a
+// song outside its step's rows (offsets not monotone) reads its rows directly.
+// The host takes it once every wave runs >= 4 steps (else k_segment_mean).
+template <int C, int DT, int ODT>
+__global__ __launch_bounds__(256) void k_segment_mean_tiles(const void* __restrict__ frames,
+                                                            const int64_t* __restrict__ offsets, int64_t N,
+                                                            void* __restrict__ out, int64_t ldo) {
+    constexpr int G = 64 / C, EB = DT == kF64 ? 8 : 4, TB = 16384;
+    static_assert(64 % C == 0 && (C * EB) % 16 == 0, "C lanes per song, 16-B rows");
+    __shared__ __attribute__((aligned(16))) char tiles[4][TB];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sg = lane / C, c = lane - sg * C;
+    const int64_t step = (int64_t)gridDim.x * 4 * G;
+    for (int64_t t0 = ((int64_t)blockIdx.x * 4 + w) * G; t0 < N; t0 += step) {
+        const int64_t n = t0 + sg;
+        const bool live = n < N;
+        const int64_t f0 = live ? offsets[n] : 0, f1 = live ? offsets[n + 1] : 0;
+        const int64_t R0 = offsets[t0], R1 = offsets[t0 + G < N ? t0 + G : N];
+        CE_DASSERT(f0 >= 0 && f0 <= f1);
+        double s = 0.0;  // np.add.reduce identity
+        int cnt = 0;
+        if (__all(!live || (f0 >= R0 && f1 <= R1))) {  // wave-uniform
+            tile_song_sum<C, EB, TB>(static_cast<const char*>(frames), R0, R1, f0, f1, lane, c, tiles[w], s, cnt);
+        } else {
+            for (int64_t f = f0; f < f1; ++f) {
+                const double v = DT == kF64 ? static_cast<const double*>(frames)[f * C + c]
+                                            : (double)static_cast<const float*>(frames)[f * C + c];
+                if (v == v) {
+                    s += v;
+                    ++cnt;
+                }
+            }
+        }
+        if (live) {
+            double m = cnt ? s / (double)cnt : __longlong_as_double(0x7ff8000000000000ll);
+            if constexpr (DT == kF32) m = (double)(float)m;  // the float32 result column
+            if constexpr (ODT == kF32)
+                static_cast<float*>(out)[n * ldo + c] = (float)m;
+            else
+                static_cast<double*>(out)[n * ldo + c] = m;
+        }
+    }
 }
 
 }  // namespace ce

@@ -728,6 +728,48 @@ def test_segment_mean_vs_restatement(ce, dt, grouped):
     assert np.array_equal(slot[1].cpu().numpy(), exp.astype(np.float64), equal_nan=True)
 
 
+@pytest.mark.parametrize("C,dt", [(4, np.float64), (2, np.float64), (8, np.float32), (4, np.float32)])
+def test_segment_mean_tiles_large(ce, C, dt):
+    """The LDS-DMA tile kernel (k_segment_mean_tiles: grouped dense rows, taken
+    once every wave runs >= 4 steps) at 300k ragged songs (1..15 frames, 1 % of
+    them 40, spanning tiles): NaN cells, all-NaN songs, bit-exact vs the restatement,
+    into a strided f64 stack slot too."""
+    from oracle.ce_oracle import ref_group_mean
+
+    rng = np.random.default_rng(C + (dt == np.float32))
+    N = 300_000
+    sizes = rng.integers(1, 16, N)
+    sizes[rng.random(N) < 0.01] = 40  # a few long songs span tiles
+    s_id = np.repeat(np.arange(N), sizes)
+    F = len(s_id)
+    vals = rng.random((F, C)).astype(dt)
+    vals[rng.random((F, C)) < 0.05] = np.nan
+    vals[np.isin(s_id, np.arange(0, N, 997)), 0] = np.nan  # all-NaN columns
+    exp, keys = ref_group_mean(vals, s_id)
+    uniq, offsets, perm = ce.song_groups(s_id)
+    assert perm is None and len(uniq) == N
+    got = ce.ops.segment_mean(dev(vals), dev(offsets))
+    assert np.array_equal(got.cpu().numpy(), exp, equal_nan=True)
+    slot = torch.empty((2, N, C), dtype=torch.float64, device="cuda")
+    ce.ops.segment_mean(dev(vals), dev(offsets), out=slot[1])
+    assert np.array_equal(slot[1].cpu().numpy(), exp.astype(np.float64), equal_nan=True)
+
+
+def test_segment_mean_tiles_forced_vs_restatement():
+    """test_segment_mean_vs_restatement's small cases (1608 songs, NaN, all-NaN
+    songs, f32 rounding) with the tile kernel forced by CE_AMD_FRAMES_DMA=1 in
+    a child process; shuffled cases keep the thread-per-cell kernel."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, CE_AMD_FRAMES_DMA="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.abspath(__file__), "-q", "-x", "-m", "gpu",
+                        "-k", "segment_mean_vs_restatement", "-p", "no:cacheprovider"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout
+
+
 def test_frames_to_selection(ce):
     """amg_test.py:426-445 end to end: three frame-level members (f64, f64,
     f32 -- GNB/SGD/XGB predict_proba over X_train rows) grouped per song on the
